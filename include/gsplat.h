@@ -1,0 +1,177 @@
+/*
+ * gsplat.h -- C ABI of libgsplat_hip.so, the MI355X (gfx950) Gaussian-splat hot path.
+ *
+ * This is the drop-in boundary for the reference's GL dispatch
+ * (thomas-chernaik/OpenGLGaussianSplattingRenderer; paths below are relative to it).
+ * Every entry point names the reference interface it replaces.  Plain pointers and
+ * sizes only; no torch / HIP types.  All functions return GS_OK (0) or a negative
+ * GS_ERR_* code; gs_last_error() gives the message (the reference prints and
+ * continues, src/sort.cpp:150-154, src/Splats.cpp:245-249 -- the C++ facade in
+ * gsplat_splats.hpp prints the same messages).
+ *
+ * Threading: one gs_ctx per GPU; a ctx is not thread-safe; different ctxs may be
+ * driven from different host threads.  Work is enqueued on the ctx's own HIP stream.
+ * Ownership: the caller owns every host buffer it passes (copied on upload); a
+ * gs_scene owns its device arrays; a gs_ctx owns its stream and frame scratch.
+ */
+#ifndef GSPLAT_H
+#define GSPLAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GS_OK 0
+#define GS_ERR_INVALID (-1)  /* bad argument (null pointer, n < 0, ...) */
+#define GS_ERR_HIP (-2)      /* HIP runtime error (no device, launch failure, ...) */
+#define GS_ERR_IO (-3)       /* file could not be opened / parsed */
+#define GS_ERR_NOMEM (-4)    /* device or host allocation failed */
+#define GS_ERR_STATE (-5)    /* stage called out of order (e.g. gs_draw before gs_sort) */
+
+/* render flags */
+#define GS_FLAG_CLEAN 1u     /* fix the reference's deterministic quirks */
+#define GS_FLAG_FAST_EXP 2u  /* blend uses the hardware v_exp_f32 (tolerance parity) instead of
+                                the bit-exact polynomial exp shared with the oracle's definition */
+#define GS_FLAG_TIMING 4u    /* record per-stage hipEvent timings into gs_frame_stats */
+#define GS_FLAG_NO_CULL 8u   /* disable the (exactness-preserving) per-block entry cull */
+
+typedef struct gs_ctx gs_ctx;
+typedef struct gs_scene gs_scene;
+
+/* Uniforms of Splats::gpuRender (include/Splats.h:122, src/Splats.cpp:587-597):
+ * glm::mat4 is column-major float[16]; tan_fov_x/y are passed exactly as main.cpp:62-64
+ * passes them (x := Camera::getTanFovy(), y := getTanFovx()). */
+typedef struct gs_uniforms {
+    float view[16];
+    float vp[16];
+    int32_t width, height;
+    float focal_x, focal_y;
+    float tan_fov_x, tan_fov_y;
+} gs_uniforms;
+
+typedef struct gs_frame_stats {
+    int64_t num_splats;   /* N */
+    int64_t visible;      /* V: main entries (on-screen, det != 0) */
+    int64_t duplicates;   /* D: extra (splat, tile) entries -- uncapped (Q12 resolved) */
+    int64_t entries;      /* E = V + D: sorted entries */
+    float ms_preprocess;  /* GS_FLAG_TIMING only (hipEvent, device time) */
+    float ms_sort;
+    float ms_bins;
+    float ms_draw;
+    float ms_total;
+} gs_frame_stats;
+
+/* Camera restatement (src/Camera.cpp:19-65,181-212, include/Camera.h:13-66) */
+typedef struct gs_camera {
+    float position[3];   /* Camera(x,y,z) */
+    float rotation[3];   /* degrees, rotateUp adds to [0], rotateRight to [1] */
+    float fovy;          /* 60 */
+    float near_plane;    /* 0.1 */
+    float far_plane;     /* 10000 */
+    int32_t width, height;
+} gs_camera;
+
+/* ---------------------------------------------------------------- library */
+const char *gs_version(void);
+int gs_device_count(int *count);
+/* last error message of this ctx (ctx == NULL: of the calling thread) */
+const char *gs_last_error(const gs_ctx *ctx);
+
+/* --------------------------------------------------------------- context
+ * Replaces the GL context + program objects: Splats::loadShaders (src/Splats.cpp:156-172),
+ * createAndLinkSortAndHistogramShaders (src/sort.cpp:15-124). */
+int gs_ctx_create(int device, gs_ctx **out);
+void gs_ctx_destroy(gs_ctx *ctx);
+int gs_sync(gs_ctx *ctx);                    /* glFinish (src/Splats.cpp:595) */
+void *gs_stream(gs_ctx *ctx);                /* the ctx's hipStream_t, for interop */
+
+/* device memory helpers (callers without their own allocator, e.g. ctypes tests) */
+int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr);
+int gs_free(gs_ctx *ctx, void *dptr);
+int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes);
+int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes);
+int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* ------------------------------------------------------- host: loader etc. */
+/* src/Splats.cpp:250-262: N from the header ("element vertex N" on line 3) */
+int gs_ply_count(const char *path, int *n);
+/* src/Splats.cpp:174-344 loadSplats: means4 (x,y,z,1), colours4 ((0.5+C0*f_dc)*255,..,1),
+ * opacity sigmoid, scales3 exp, rots4 normalised (rot_0..rot_3).  Any output may be NULL. */
+int gs_ply_load(const char *path, int n, float *means4, float *colours4, float *opacity,
+                float *scales3, float *rots4);
+/* tests/plyFileGenerator.py:155-249 save_ply byte layout (raw colours into f_dc, logit
+ * opacity, log scale, zero normals / SH).  means3, rots4, scales3, opac, colours3 as given. */
+int gs_ply_write(const char *path, int n, const float *means3, const float *rots4,
+                 const float *scales3, const float *opacities, const float *colours3);
+/* same activations as the loader, from raw (pre-activation) SoA records:
+ * f_dc3, opacity logit, log-scale3, raw quaternion4 -> colours4, opacity, scales3, rots4 */
+int gs_activate(int n, const float *f_dc3, const float *opacity_logit, const float *log_scale3,
+                const float *rot_raw4, float *colours4, float *opacity, float *scales3,
+                float *rots4);
+/* src/Splats.cpp:414-479 computeCovarianceMatrices: [S00,S01,S02,S11,S12,S22] per splat */
+int gs_covariance3d(int n, const float *scales3, const float *rots4, float *cov6);
+/* Camera getters (src/Camera.cpp): view, projection, focal x/y, getTanFovx/y (degree-
+ * argument quirk Q1 kept), and the uniforms as main.cpp:62-64 passes them (Q2 swap). */
+int gs_camera_update(const gs_camera *cam, float view16[16], float proj16[16], float *focal_x,
+                     float *focal_y, float *tan_fovx_getter, float *tan_fovy_getter);
+int gs_camera_uniforms(const gs_camera *cam, gs_uniforms *out);
+
+/* ---------------------------------------------------------------- scene
+ * Splats::loadToGPU (src/Splats.cpp:61-154): host vectors copied to device SoA. */
+int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6,
+                    const float *opacity, const float *colours4, gs_scene **out);
+void gs_scene_destroy(gs_scene *scene);
+int gs_scene_count(const gs_scene *scene);
+
+/* ---------------------------------------------------------------- frame
+ * Splats::gpuRender (src/Splats.cpp:587-597) = preprocess -> sort -> bins -> draw.
+ * out_rgba8: W*H*4 bytes, row y = GL row y (bottom-up as in the reference texture);
+ * on the host (out_on_device = 0) or a device pointer (1).  stats may be NULL. */
+int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
+              void *out_rgba8, int out_on_device, gs_frame_stats *stats);
+
+/* stage-level entry points mirroring the reference's Splats methods */
+/* Splats::preprocess (src/Splats.cpp:542-585) + the per-splat entry emission.
+ * Replaces preprocess.glsl and the atomic-counter readback (:579-583). */
+int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
+                  gs_frame_stats *stats);
+/* Splats::sort (src/Splats.cpp:346-354): stable sort of the frame's entries by key bits */
+int gs_sort(gs_ctx *ctx);
+/* Splats::computeBins (src/Splats.cpp:481-512, countBins.glsl, prefixBins.glsl) */
+int gs_compute_bins(gs_ctx *ctx);
+/* Splats::draw (src/Splats.cpp:356-381, draw.glsl): tile_w/tile_h as gpuRender passes
+ * them (float(W)/16.f, float(H)/16.f) */
+int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w,
+            float tile_h, uint32_t flags, void *out_rgba8, int out_on_device);
+
+/* frame-state readback for parity tests (host buffers; counts in elements) */
+#define GS_READ_KEYS 1      /* uint32[E] sorted (after gs_sort) or emitted key bits */
+#define GS_READ_VALS 2      /* uint32[E] splat index per entry */
+#define GS_READ_BINS 3      /* uint32[256] inclusive tile ends (after gs_compute_bins) */
+#define GS_READ_MEANS2D 4   /* float[2N] */
+#define GS_READ_CONICS 5    /* float[4N] conic.xyz + opacity */
+#define GS_READ_CULLBOX 6   /* float[4N] per-splat pixel box used by the block cull */
+int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count);
+
+/* ------------------------------------------------------------- radix sort */
+/* GPURadixSort (include/sort.h:18-20, src/sort.cpp:139-203): stable argsort of float
+ * keys by floatBitsToUint; d_order (int32[n]) is read as the initial order and
+ * overwritten with the sorted order; d_keys are not moved (read as keys[order[i]]). */
+int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n);
+/* stable sort of (key, value) pairs in place by the 32-bit key */
+int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n);
+/* PadBuffer (include/sort.h:23, src/sort.cpp:127-137) */
+int gs_pad_buffer(int size, int unit_width);
+
+/* time the last launch of a kernel class in ms (GS_FLAG_TIMING frames / sorts) */
+#define GS_KERNEL_DRAW 1
+#define GS_KERNEL_SORT 2
+int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

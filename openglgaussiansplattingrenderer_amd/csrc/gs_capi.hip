@@ -1,0 +1,550 @@
+// gs_capi.hip -- the extern "C" boundary (include/gsplat.h) and the frame orchestration
+// that replaces Splats::gpuRender's GL dispatch (src/Splats.cpp:542-597).
+#include "gs_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+struct gs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // per-splat frame buffers (sized by the largest scene rendered so far)
+    int n_cap = 0;
+    float2 *m2d = nullptr;
+    float4 *conic = nullptr;
+    float4 *cullbox = nullptr;
+    int4 *rec = nullptr;
+    uint2 *blocksum = nullptr;
+    uint32_t *totals = nullptr;      // device [4]
+    uint32_t *h_totals = nullptr;    // pinned [4]
+    // entries
+    int64_t e_cap = 0;
+    uint32_t *keys = nullptr, *vals = nullptr;
+    gs::SortScratch sort;
+    // bins
+    uint32_t *bin_counts = nullptr;  // [256]
+    uint32_t *bins = nullptr;        // [256]
+    // output staging (host-destination renders)
+    uint32_t *img = nullptr;
+    size_t img_cap = 0;
+    // argsort key scratch
+    uint32_t *ask = nullptr;
+    size_t ask_cap = 0;
+    // frame state
+    int stage = 0;  // 0 none, 1 preprocessed, 2 sorted, 3 binned
+    int n = 0;
+    int64_t V = 0, D = 0, E = 0;
+    uint32_t flags = 0;
+    // timing
+    hipEvent_t ev[8] = {};
+    float last_draw_ms = 0.f, last_sort_ms = 0.f;
+};
+
+struct gs_scene {
+    gs_ctx *ctx = nullptr;
+    int n = 0;
+    float *soa = nullptr;       // mx | my | mz | cov0..cov5 | opacity  (10 planes of n floats)
+    float4 *colour = nullptr;   // (r,g,b,1)
+};
+
+namespace gs {
+
+static thread_local std::string t_err;
+
+int set_error(gs_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    t_err = msg;
+    return code;
+}
+
+}  // namespace gs
+
+using gs::set_error;
+
+#define GS_HIP(ctx, call)                                                                                    \
+    do {                                                                                                     \
+        hipError_t e_ = (call);                                                                              \
+        if (e_ != hipSuccess)                                                                                \
+            return set_error((ctx), GS_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_));         \
+    } while (0)
+
+namespace {
+
+int use_device(gs_ctx *ctx) {
+    GS_HIP(ctx, hipSetDevice(ctx->device));
+    return GS_OK;
+}
+
+template <typename T>
+int grow(gs_ctx *ctx, T *&p, size_t count) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    GS_HIP(ctx, hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
+    return GS_OK;
+}
+
+int ensure_splats(gs_ctx *ctx, int n) {
+    if (n <= ctx->n_cap) return GS_OK;
+    const int cap = n;
+    const int nb = (cap + 255) / 256;
+    int rc;
+    if ((rc = grow(ctx, ctx->m2d, cap)) || (rc = grow(ctx, ctx->conic, cap)) || (rc = grow(ctx, ctx->cullbox, cap)) ||
+        (rc = grow(ctx, ctx->rec, cap)) || (rc = grow(ctx, ctx->blocksum, nb)))
+        return rc;
+    ctx->n_cap = cap;
+    return GS_OK;
+}
+
+int ensure_entries(gs_ctx *ctx, int64_t e) {
+    if (e <= ctx->e_cap) return GS_OK;
+    const int64_t cap = e + e / 4 + 4096;
+    int rc;
+    if ((rc = grow(ctx, ctx->keys, (size_t)cap)) || (rc = grow(ctx, ctx->vals, (size_t)cap))) return rc;
+    ctx->e_cap = cap;
+    return GS_OK;
+}
+
+gs::FrameDev frame_dev(gs_ctx *ctx) {
+    gs::FrameDev f;
+    f.m2d = ctx->m2d;
+    f.conic = ctx->conic;
+    f.cullbox = ctx->cullbox;
+    f.rec = ctx->rec;
+    f.blocksum = ctx->blocksum;
+    f.totals = ctx->totals;
+    return f;
+}
+
+gs::SceneDev scene_dev(const gs_scene *s) {
+    gs::SceneDev d;
+    const size_t n = (size_t)s->n;
+    d.n = s->n;
+    d.mx = s->soa;
+    d.my = s->soa + n;
+    d.mz = s->soa + 2 * n;
+    d.cov = s->soa + 3 * n;
+    d.opacity = s->soa + 9 * n;
+    d.colour = s->colour;
+    return d;
+}
+
+bool timing(const gs_ctx *ctx) { return (ctx->flags & GS_FLAG_TIMING) != 0; }
+
+}  // namespace
+
+extern "C" {
+
+const char *gs_version(void) { return "gsplat-mi355x 0.1 (gfx950)"; }
+
+const char *gs_last_error(const gs_ctx *ctx) { return ctx ? ctx->err.c_str() : gs::t_err.c_str(); }
+
+int gs_device_count(int *count) {
+    if (!count) return set_error(nullptr, GS_ERR_INVALID, "count is null");
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return GS_OK;
+}
+
+int gs_ctx_create(int device, gs_ctx **out) {
+    if (!out) return set_error(nullptr, GS_ERR_INVALID, "out is null");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+        return set_error(nullptr, GS_ERR_HIP, "no HIP device available (libgsplat_hip needs an MI355X)");
+    if (device < 0 || device >= count) return set_error(nullptr, GS_ERR_INVALID, "device index out of range");
+    gs_ctx *ctx = new gs_ctx();
+    ctx->device = device;
+    int rc;
+    auto fail = [&](int code) {
+        gs_ctx_destroy(ctx);
+        return code;
+    };
+    if ((rc = use_device(ctx))) return fail(rc);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
+        return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
+    if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess)
+        return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
+    for (auto &e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
+    *out = ctx;
+    return GS_OK;
+}
+
+void gs_ctx_destroy(gs_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    void *bufs[] = {ctx->m2d, ctx->conic, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
+                    ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (ctx->h_totals) (void)hipHostFree(ctx->h_totals);
+    gs::sort_free(ctx->sort);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int gs_sync(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GS_OK;
+}
+
+void *gs_stream(gs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr) {
+    if (!ctx || !dptr) return set_error(ctx, GS_ERR_INVALID, "null argument");
+    if (int rc = use_device(ctx)) return rc;
+    GS_HIP(ctx, hipMalloc(dptr, std::max<size_t>(bytes, 1)));
+    return GS_OK;
+}
+int gs_free(gs_ctx *ctx, void *dptr) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (dptr) GS_HIP(ctx, hipFree(dptr));
+    return GS_OK;
+}
+int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GS_OK;
+}
+int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GS_OK;
+}
+int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    GS_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return GS_OK;
+}
+
+// ------------------------------------------------------------------ host side
+int gs_ply_count(const char *path, int *n) {
+    if (!path || !n) return set_error(nullptr, GS_ERR_INVALID, "null argument");
+    return gs::ply_count(path, n);
+}
+int gs_ply_load(const char *path, int n, float *means4, float *colours4, float *opacity, float *scales3,
+                float *rots4) {
+    if (!path || n < 0) return set_error(nullptr, GS_ERR_INVALID, "bad argument");
+    return gs::ply_load(path, n, means4, colours4, opacity, scales3, rots4);
+}
+int gs_ply_write(const char *path, int n, const float *means3, const float *rots4, const float *scales3,
+                 const float *opacities, const float *colours3) {
+    if (!path || n < 0 || (n > 0 && (!means3 || !rots4 || !scales3 || !opacities || !colours3)))
+        return set_error(nullptr, GS_ERR_INVALID, "bad argument");
+    return gs::ply_write(path, n, means3, rots4, scales3, opacities, colours3);
+}
+int gs_activate(int n, const float *f_dc3, const float *opacity_logit, const float *log_scale3, const float *rot_raw4,
+                float *colours4, float *opacity, float *scales3, float *rots4) {
+    if (n < 0 || (n > 0 && (!f_dc3 || !opacity_logit || !log_scale3 || !rot_raw4)))
+        return set_error(nullptr, GS_ERR_INVALID, "bad argument");
+    return gs::activate(n, f_dc3, opacity_logit, log_scale3, rot_raw4, colours4, opacity, scales3, rots4);
+}
+int gs_covariance3d(int n, const float *scales3, const float *rots4, float *cov6) {
+    if (n < 0 || (n > 0 && (!scales3 || !rots4 || !cov6))) return set_error(nullptr, GS_ERR_INVALID, "bad argument");
+    return gs::covariance3d(n, scales3, rots4, cov6);
+}
+int gs_camera_update(const gs_camera *cam, float view16[16], float proj16[16], float *focal_x, float *focal_y,
+                     float *tan_fovx_getter, float *tan_fovy_getter) {
+    if (!cam || cam->height == 0) return set_error(nullptr, GS_ERR_INVALID, "bad camera");
+    return gs::camera_update(cam, view16, proj16, focal_x, focal_y, tan_fovx_getter, tan_fovy_getter);
+}
+int gs_camera_uniforms(const gs_camera *cam, gs_uniforms *out) {
+    if (!cam || !out || cam->height == 0) return set_error(nullptr, GS_ERR_INVALID, "bad camera");
+    return gs::camera_uniforms(cam, out);
+}
+int gs_pad_buffer(int size, int unit_width) {
+    // src/sort.cpp:127-137
+    if (unit_width <= 0) return 0;
+    if (size % unit_width == 0) return 0;
+    return unit_width - (size % unit_width);
+}
+
+// ---------------------------------------------------------------------- scene
+int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, const float *opacity,
+                    const float *colours4, gs_scene **out) {
+    if (!ctx || !out || n < 0 || (n > 0 && (!means4 || !cov6 || !opacity || !colours4)))
+        return set_error(ctx, GS_ERR_INVALID, "gs_scene_create: bad argument");
+    *out = nullptr;
+    if (int rc = use_device(ctx)) return rc;
+    // host AoS (reference layout) -> device SoA planes
+    const size_t nn = (size_t)n;
+    std::vector<float> soa(10 * std::max<size_t>(nn, 1));
+    for (size_t i = 0; i < nn; ++i) {
+        soa[i] = means4[4 * i + 0];
+        soa[nn + i] = means4[4 * i + 1];
+        soa[2 * nn + i] = means4[4 * i + 2];
+        for (int c = 0; c < 6; ++c) soa[(3 + c) * nn + i] = cov6[6 * i + c];
+        soa[9 * nn + i] = opacity[i];
+    }
+    gs_scene *s = new gs_scene();
+    s->ctx = ctx;
+    s->n = n;
+    if (hipMalloc(&s->soa, soa.size() * 4) != hipSuccess ||
+        hipMalloc(&s->colour, std::max<size_t>(nn, 1) * sizeof(float4)) != hipSuccess) {
+        gs_scene_destroy(s);
+        return set_error(ctx, GS_ERR_NOMEM, "gs_scene_create: out of device memory");
+    }
+    GS_HIP(ctx, hipMemcpyAsync(s->soa, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (n > 0) GS_HIP(ctx, hipMemcpyAsync(s->colour, colours4, nn * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = s;
+    return GS_OK;
+}
+
+void gs_scene_destroy(gs_scene *scene) {
+    if (!scene) return;
+    if (scene->ctx) (void)hipSetDevice(scene->ctx->device);
+    if (scene->soa) (void)hipFree(scene->soa);
+    if (scene->colour) (void)hipFree(scene->colour);
+    delete scene;
+}
+
+int gs_scene_count(const gs_scene *scene) { return scene ? scene->n : -1; }
+
+// ---------------------------------------------------------------------- frame
+int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, gs_frame_stats *stats) {
+    if (!ctx || !scene || !u) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: null argument");
+    if (scene->ctx != ctx) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: scene belongs to another ctx");
+    if (u->width <= 0 || u->height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: bad resolution");
+    if (int rc = use_device(ctx)) return rc;
+    ctx->flags = flags;
+    const int n = scene->n;
+    if (int rc = ensure_splats(ctx, n)) return rc;
+    gs::PreParams P;
+    std::memcpy(P.view, u->view, sizeof(P.view));
+    std::memcpy(P.vp, u->vp, sizeof(P.vp));
+    P.W = (uint32_t)u->width;
+    P.H = (uint32_t)u->height;
+    P.fx = u->focal_x;
+    P.fy = u->focal_y;
+    P.tan_fov_x = u->tan_fov_x;
+    P.tan_fov_y = u->tan_fov_y;
+    P.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
+    if (!P.clean) {  // preprocess.glsl:143-144 integer screen/16 (Q4)
+        P.tile_w = (float)(P.W / 16);
+        P.tile_h = (float)(P.H / 16);
+    } else {
+        P.tile_w = (float)u->width / 16.f;
+        P.tile_h = (float)u->height / 16.f;
+    }
+    P.n = n;
+    const gs::FrameDev fr = frame_dev(ctx);
+    const int nb = (n + 255) / 256;
+    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    GS_HIP(ctx, hipMemsetAsync(ctx->totals, 0, 16, ctx->stream));
+    gs::launch_preprocess(ctx->stream, P, scene_dev(scene), fr);
+    if (nb > 0) gs::launch_scan_blocksums(ctx->stream, fr, nb);
+    GS_HIP(ctx, hipGetLastError());
+    // E is needed on the host to size the sort (the reference maps its atomic counter back
+    // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
+    GS_HIP(ctx, hipMemcpyAsync(ctx->h_totals, ctx->totals, 8, hipMemcpyDeviceToHost, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->V = ctx->h_totals[0];
+    ctx->D = ctx->h_totals[1];
+    ctx->E = ctx->V + ctx->D;
+    if (ctx->E >= ((int64_t)1 << 31)) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: more than 2^31 entries");
+    if (int rc = ensure_entries(ctx, ctx->E)) return rc;
+    gs::launch_emit(ctx->stream, n, fr, ctx->keys, ctx->vals);
+    GS_HIP(ctx, hipGetLastError());
+    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    ctx->n = n;
+    ctx->stage = 1;
+    if (stats) {
+        stats->num_splats = n;
+        stats->visible = ctx->V;
+        stats->duplicates = ctx->D;
+        stats->entries = ctx->E;
+    }
+    return GS_OK;
+}
+
+int gs_sort(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_sort: call gs_preprocess first");
+    if (int rc = use_device(ctx)) return rc;
+    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, ctx->E, ctx->err)) return set_error(ctx, rc, ctx->err);
+    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    ctx->stage = 2;
+    return GS_OK;
+}
+
+int gs_compute_bins(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (ctx->stage < 2) return set_error(ctx, GS_ERR_STATE, "gs_compute_bins: call gs_sort first");
+    if (int rc = use_device(ctx)) return rc;
+    GS_HIP(ctx, hipMemsetAsync(ctx->bin_counts, 0, 256 * 4, ctx->stream));
+    gs::launch_bins(ctx->stream, ctx->keys, ctx->E, ctx->bin_counts, ctx->bins);
+    GS_HIP(ctx, hipGetLastError());
+    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    ctx->stage = 3;
+    return GS_OK;
+}
+
+int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w, float tile_h, uint32_t flags,
+            void *out_rgba8, int out_on_device) {
+    if (!ctx || !scene || !out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_draw: null argument");
+    if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_draw: call gs_compute_bins first");
+    if (width <= 0 || height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_draw: bad resolution");
+    if (scene->n != ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_draw: scene differs from the preprocessed one");
+    if (int rc = use_device(ctx)) return rc;
+    const bool clean = (flags & GS_FLAG_CLEAN) != 0;
+    gs::DrawParams P;
+    P.W = width;
+    P.H = height;
+    P.E = (int32_t)ctx->E;
+    P.clean = clean ? 1 : 0;
+    P.no_cull = (flags & GS_FLAG_NO_CULL) ? 1 : 0;
+    // Q9: the reference dispatches (W/32) x (H/32) workgroups of 32x32 pixels
+    const int coverW = clean ? width : (width / 32) * 32;
+    const int coverH = clean ? height : (height / 32) * 32;
+    // tile pixel ranges with the kernel's own float formula: tileX = int(float(x) / tile_w)
+    auto bounds = [](int cover, float tsz, int32_t *b) {
+        for (int t = 0; t <= gs::kTiles; ++t) b[t] = cover;
+        int prev = -1;
+        for (int x = 0; x < cover; ++x) {
+            int tt = (int)((float)x / tsz);
+            tt = std::min(std::max(tt, 0), gs::kTiles);
+            for (int q = prev + 1; q <= tt && q <= gs::kTiles; ++q) b[q] = x;
+            prev = std::max(prev, tt);
+        }
+        b[0] = 0;
+    };
+    bounds(coverW, tile_w, P.xb);
+    bounds(coverH, tile_h, P.yb);
+    int mw = 0, mh = 0;
+    for (int t = 0; t < gs::kTiles; ++t) {
+        mw = std::max(mw, P.xb[t + 1] - P.xb[t]);
+        mh = std::max(mh, P.yb[t + 1] - P.yb[t]);
+    }
+    P.nbx = (mw + 15) / 16;
+    P.nby = (mh + 15) / 16;
+    const size_t npx = (size_t)width * height;
+    uint32_t *dst = (uint32_t *)out_rgba8;
+    if (!out_on_device) {
+        if (npx > ctx->img_cap) {
+            if (int rc = grow(ctx, ctx->img, npx)) return rc;
+            ctx->img_cap = npx;
+        }
+        dst = ctx->img;
+    }
+    if (coverW < width || coverH < height) GS_HIP(ctx, hipMemsetAsync(dst, 0, npx * 4, ctx->stream));
+    GS_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), scene->colour,
+                    dst);
+    GS_HIP(ctx, hipGetLastError());
+    GS_HIP(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
+    if (!out_on_device) {
+        GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
+        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return GS_OK;
+}
+
+int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
+              int out_on_device, gs_frame_stats *stats) {
+    if (!ctx || !scene || !u || !out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_render: null argument");
+    int rc;
+    if ((rc = gs_preprocess(ctx, scene, u, flags, stats))) return rc;
+    if ((rc = gs_sort(ctx))) return rc;
+    if ((rc = gs_compute_bins(ctx))) return rc;
+    // src/Splats.cpp:596 draw(width, height, float(width) / 16.f, float(height) / 16.f)
+    if ((rc = gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
+                      out_rgba8, out_on_device)))
+        return rc;
+    if (timing(ctx)) {
+        GS_HIP(ctx, hipEventSynchronize(ctx->ev[6]));
+        float a = 0, b = 0, c = 0, d = 0, t = 0;
+        (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
+        (void)hipEventElapsedTime(&b, ctx->ev[2], ctx->ev[3]);
+        (void)hipEventElapsedTime(&c, ctx->ev[3], ctx->ev[4]);
+        (void)hipEventElapsedTime(&d, ctx->ev[5], ctx->ev[6]);
+        (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[6]);
+        ctx->last_draw_ms = d;
+        ctx->last_sort_ms = b;
+        if (stats) {
+            stats->ms_preprocess = a;
+            stats->ms_sort = b;
+            stats->ms_bins = c;
+            stats->ms_draw = d;
+            stats->ms_total = t;
+        }
+    }
+    return GS_OK;
+}
+
+int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
+    if (!ctx || (!host_dst && count)) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: null argument");
+    if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: no frame");
+    if (int rc = use_device(ctx)) return rc;
+    const void *src = nullptr;
+    size_t avail = 0, esz = 4;
+    switch (what) {
+    case GS_READ_KEYS: src = ctx->keys; avail = (size_t)ctx->E; break;
+    case GS_READ_VALS: src = ctx->vals; avail = (size_t)ctx->E; break;
+    case GS_READ_BINS:
+        if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");
+        src = ctx->bins; avail = 256; break;
+    case GS_READ_MEANS2D: src = ctx->m2d; avail = 2 * (size_t)ctx->n; break;
+    case GS_READ_CONICS: src = ctx->conic; avail = 4 * (size_t)ctx->n; break;
+    case GS_READ_CULLBOX: src = ctx->cullbox; avail = 4 * (size_t)ctx->n; break;
+    default: return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: unknown buffer");
+    }
+    if (count > avail) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");
+    if (count) {
+        GS_HIP(ctx, hipMemcpyAsync(host_dst, src, count * esz, hipMemcpyDeviceToHost, ctx->stream));
+        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    return GS_OK;
+}
+
+// ---------------------------------------------------------------- radix sort
+int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n) {
+    if (!ctx || (n > 0 && (!d_keys || !d_order)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_argsort_f32: bad argument");
+    if (n <= 1) return GS_OK;
+    if (int rc = use_device(ctx)) return rc;
+    if ((size_t)n > ctx->ask_cap) {
+        if (int rc = grow(ctx, ctx->ask, (size_t)n + (size_t)n / 4)) return rc;
+        ctx->ask_cap = (size_t)n + (size_t)n / 4;
+    }
+    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    gs::launch_gather_keys(ctx->stream, d_keys, d_order, ctx->ask, n);
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->ask, (uint32_t *)d_order, n, ctx->err))
+        return set_error(ctx, rc, ctx->err);
+    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    return GS_OK;
+}
+
+int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n) {
+    if (!ctx || (n > 0 && (!d_keys || !d_vals)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_sort_pairs_u32: bad argument");
+    if (int rc = use_device(ctx)) return rc;
+    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, d_keys, d_vals, n, ctx->err)) return set_error(ctx, rc, ctx->err);
+    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    return GS_OK;
+}
+
+int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
+    if (!ctx || !ms) return set_error(ctx, GS_ERR_INVALID, "null argument");
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (kernel == GS_KERNEL_DRAW) GS_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[5], ctx->ev[6]));
+    else if (kernel == GS_KERNEL_SORT) GS_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[2], ctx->ev[3]));
+    else return set_error(ctx, GS_ERR_INVALID, "unknown kernel");
+    return GS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// gs_internal.hpp -- declarations shared by the library's translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/gsplat.h"
+
+namespace gs {
+
+// error plumbing: every C entry point returns a status and records a message
+int set_error(gs_ctx *ctx, int code, const std::string &msg);
+
+// host side (gs_host.cpp)
+int ply_count(const char *path, int *n);
+int ply_load(const char *path, int n, float *means4, float *colours4, float *opacity, float *scales3,
+             float *rots4);
+int ply_write(const char *path, int n, const float *means3, const float *rots4, const float *scales3,
+              const float *opacities, const float *colours3);
+int activate(int n, const float *f_dc3, const float *opacity_logit, const float *log_scale3,
+             const float *rot_raw4, float *colours4, float *opacity, float *scales3, float *rots4);
+int covariance3d(int n, const float *scales3, const float *rots4, float *cov6);
+int camera_update(const gs_camera *cam, float view16[16], float proj16[16], float *focal_x, float *focal_y,
+                  float *tan_fovx_getter, float *tan_fovy_getter);
+int camera_uniforms(const gs_camera *cam, gs_uniforms *u);
+
+// ---------------------------------------------------------------- device side
+constexpr int kTiles = 16;  // the reference's fixed 16x16 coarse grid (preprocess.glsl:143-153)
+
+// Per-frame uniforms of the preprocess kernel (preprocess.glsl:18-37)
+struct PreParams {
+    float view[16];
+    float vp[16];
+    uint32_t W, H;
+    float fx, fy, tan_fov_x, tan_fov_y;
+    float tile_w, tile_h;  // int-derived (ref, Q4) or float (clean)
+    int32_t clean;
+    int32_t n;
+};
+
+// Per-frame parameters of the blend kernel (draw.glsl:38-47)
+struct DrawParams {
+    int32_t W, H;
+    int32_t E;
+    int32_t clean;
+    int32_t no_cull;
+    int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
+    int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
+    int32_t yb[kTiles + 1];
+};
+
+// radix sort scratch (gs_sort.hip)
+struct SortScratch {
+    uint32_t *keys_alt = nullptr;
+    uint32_t *vals_alt = nullptr;
+    size_t alt_cap = 0;            // elements
+    uint32_t *hist = nullptr;      // [256][nb]
+    size_t hist_cap = 0;           // elements
+    uint32_t *row_total = nullptr; // [256]
+};
+
+int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err);
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err);
+void sort_free(SortScratch &sc);
+// argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]
+void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n);
+
+// render kernels (gs_render.hip)
+struct SceneDev {
+    int n;
+    const float *mx, *my, *mz;   // SoA means
+    const float *cov;            // 6 SoA planes of n floats: [S00 | S01 | S02 | S11 | S12 | S22]
+    const float *opacity;
+    const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
+};
+struct FrameDev {
+    float2 *m2d;
+    float4 *conic;     // conic.xyz, opacity
+    float4 *cullbox;   // conservative pixel box of the alpha >= 1/255 region
+    int4 *rec;         // z01 bits, tileX, tileY (-1: no entries), packed rect
+    uint2 *blocksum;   // per-256-splat block (main, dup) sums -> exclusive offsets
+    uint32_t *totals;  // [0]=V [1]=D
+};
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr);
+void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks);
+void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals);
+void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins);
+void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
+                 const FrameDev &fr, const float4 *colour, uint32_t *out);
+
+}  // namespace gs

@@ -1,0 +1,506 @@
+// gs_render.hip -- gfx950 kernels of the frame: preprocess, entry emission, tile bins, blend.
+//
+// Reference semantics (paths relative to the reference checkout):
+//   k_preprocess  shaders/preprocess.glsl:64-190   (one lane per splat, SoA coalesced loads)
+//   k_emit        preprocess.glsl:153-188          (deterministic layout replacing the atomic
+//                                                   counter: mains [0,V), duplicates [V,V+D))
+//   k_bins_*      countBins.glsl + prefixBins.glsl
+//   k_draw        draw.glsl:70-143                 (LDS-staged per-tile lists, block cull,
+//                                                   block early exit)
+// Float expressions are written in the same order as oracle/gs_oracle.c and compiled with
+// contraction off, so means2D / conics / keys / bins match the CPU restatement bit for bit.
+#pragma clang fp contract(off)
+
+#include "gs_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace gs {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
+
+// GLSL int(float) with v_cvt_i32_f32's out-of-range behaviour (saturate, NaN -> 0),
+// written out so the compiler cannot exploit C++'s UB on out-of-range conversions.
+__device__ __forceinline__ int f2i(float f) {
+    if (f != f) return 0;
+    if (f >= 2147483648.0f) return 2147483647;
+    if (f <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)f;
+}
+
+// glm operator*(mat4, vec4): (m0*x + m1*y) + (m2*z + m3*w)
+__device__ __forceinline__ float m4v_row(const float *m, int r, float x, float y, float z, float w) {
+    return (m[0 * 4 + r] * x + m[1 * 4 + r] * y) + (m[2 * 4 + r] * z + m[3 * 4 + r] * w);
+}
+
+// glm operator*(mat3, mat3), column-major a[c][r]
+struct M3 {
+    float v[3][3];
+};
+__device__ __forceinline__ M3 mul3(const M3 &a, const M3 &b) {
+    M3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.v[c][r] = a.v[0][r] * b.v[c][0] + a.v[1][r] * b.v[c][1] + a.v[2][r] * b.v[c][2];
+    return o;
+}
+__device__ __forceinline__ M3 tr3(const M3 &a) {
+    M3 o;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) o.v[c][r] = a.v[r][c];
+    return o;
+}
+
+// exp of draw.glsl:122 -- the same definition the oracle states (Cody-Waite + degree-6
+// polynomial); every operation is an IEEE-exact-rounded one, so CPU == GPU bit for bit.
+__device__ __forceinline__ float exp_defined(float x) {
+    if (!(x >= -80.0f)) return 0.0f;
+    if (x > 80.0f) x = 80.0f;
+    const float kf = rintf(x * 1.44269504088896341f);
+    float r = x - kf * 0.693359375f;
+    r = r - kf * -2.12194440e-4f;
+    const float p = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666672f + r * (0.0416666679f +
+                    r * (0.00833333377f + r * 0.00138888892f)))));
+    const int k = (int)kf;
+    return p * u2f((uint32_t)(k + 127) << 23);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// inclusive wave scan (wave64)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// exclusive block scan over 256 threads; returns prefix, *total = block sum
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_wave, uint32_t *total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint32_t c = s_wave[w];
+        off += (w < wid) ? c : 0u;
+        tot += c;
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
+// ------------------------------------------------------------------ preprocess
+__global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    uint32_t n_main = 0, n_dup = 0;
+    if (i < P.n) {
+        const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
+        float2 m2 = make_float2(0.f, 0.f);
+        float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 box = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
+        int4 rc = make_int4(0, -1, -1, 0);
+        do {
+            // :77-78
+            float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
+            float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
+            float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
+            const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
+            const float w = fmaxf(p3, 0.0001f);
+            p0 = p0 / w;
+            p1 = p1 / w;
+            p2 = p2 / w;
+            // :80-89 cull: NDC x/y only
+            if (p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f) break;
+            // :91-94
+            float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
+            const float sz = (p2 + 1.0f) * 0.5f;
+            sx = sx * (float)P.W;
+            sy = sy * (float)P.H;
+            if (P.clean && !(sz >= 0.0f && sz <= 1.0f)) break;  // clean: near/far cull (Q6)
+            m2 = make_float2(sx, sy);
+            // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
+            const size_t n = (size_t)P.n;
+            const float c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
+            const float c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
+            const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
+            const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
+                            {P.view[8], P.view[9], P.view[10]}}};
+            // :110-116
+            float tx = m4v_row(P.view, 0, mx, my, mz, 1.0f);
+            float ty = m4v_row(P.view, 1, mx, my, mz, 1.0f);
+            const float tz = m4v_row(P.view, 2, mx, my, mz, 1.0f);
+            const float limx = -1.3f * P.tan_fov_x, limy = -1.3f * P.tan_fov_y;
+            const float txtz = tx / tz, tytz = ty / tz;
+            tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+            ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
+            // :118-128
+            const M3 J = {{{P.fx / tz, 0.0f, -(P.fx * tx) / (tz * tz)},
+                           {0.0f, P.fy / tz, -(P.fy * ty) / (tz * tz)},
+                           {0.0f, 0.0f, 0.0f}}};
+            const M3 T = mul3(tr3(W3), J);
+            M3 C = mul3(mul3(tr3(T), tr3(Sig)), T);
+            C.v[0][0] += 0.3f;
+            C.v[1][1] += 0.3f;
+            // :129-136
+            const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
+            const float det = ca * cc - cb * cb;
+            if (det == 0) break;                   // Q7: entry omitted
+            if (P.clean && !(det > 0.0f)) break;
+            const float inv = 1.0f / det;
+            const float opac = sc.opacity[i];
+            co = make_float4(cc * inv, -cb * inv, ca * inv, opac);
+            // :139-149
+            const float middle = (cc + ca) * 0.5f;
+            const float l1 = middle + sqrtf(fmaxf(0.1f, middle * middle - det));
+            const float l2 = middle - sqrtf(fmaxf(0.1f, middle * middle - det));
+            const float radius = ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+            const int minX = max(0, f2i((sx - radius) / P.tile_w));
+            const int maxX = min(15, f2i((sx + radius) / P.tile_w));
+            const int minY = max(0, f2i((sy - radius) / P.tile_h));
+            const int maxY = min(15, f2i((sy + radius) / P.tile_h));
+            // :151-155 main tile (unclamped in ref mode, Q5)
+            int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
+            if (P.clean) {
+                tileX = min(15, max(0, tileX));
+                tileY = min(15, max(0, tileY));
+            }
+            const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+            const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
+            n_main = 1;
+            n_dup = (uint32_t)(rectCount - mainInRect);
+            const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
+                                ((uint32_t)maxY << 24);
+            rc = make_int4((int)f2u(sz), tileX, tileY, (int)rp);
+
+            // Conservative pixel box of the region where alpha >= 1/255 can hold
+            // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
+            // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
+            // culling an entry outside the box never changes a pixel.
+            const float A = co.x, B = co.y, Cq = co.z;
+            const float tau = logf(255.0f * opac) + 0.05f;
+            if (!(tau > 0.0f)) {
+                // never reaches 1/255 anywhere: empty box (stays +inf,-inf)
+            } else {
+                const float detQ = A * Cq - B * B;
+                const float trq = A + Cq;
+                if (A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ) {
+                    const float hx = sqrtf(2.0f * tau * Cq / detQ) * 1.02f + 1.0f;
+                    const float hy = sqrtf(2.0f * tau * A / detQ) * 1.02f + 1.0f;
+                    box = make_float4(sx - hx, sx + hx, sy - hy, sy + hy);
+                } else {
+                    box = make_float4(-__builtin_inff(), __builtin_inff(), -__builtin_inff(), __builtin_inff());
+                }
+            }
+        } while (false);
+        fr.m2d[i] = m2;
+        fr.conic[i] = co;
+        fr.cullbox[i] = box;
+        fr.rec[i] = rc;
+    }
+    // block sums of (main, dup) for the emission offsets
+    uint32_t tot_main, tot_dup;
+    block_excl_scan256(n_main, s_wave, &tot_main);
+    block_excl_scan256(n_dup, s_wave, &tot_dup);
+    if (threadIdx.x == 0) fr.blocksum[blockIdx.x] = make_uint2(tot_main, tot_dup);
+}
+
+// exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1]
+__global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblocks) {
+    __shared__ uint32_t s_w0[16], s_w1[16];
+    __shared__ uint32_t s_carry[2];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry[0] = s_carry[1] = 0;
+    __syncthreads();
+    for (int base = 0; base < nblocks; base += 1024) {
+        const int i = base + threadIdx.x;
+        const uint2 v = (i < nblocks) ? fr.blocksum[i] : make_uint2(0, 0);
+        const uint32_t i0 = wave_incl_scan(v.x), i1 = wave_incl_scan(v.y);
+        if (lane == 63) {
+            s_w0[wid] = i0;
+            s_w1[wid] = i1;
+        }
+        __syncthreads();
+        uint32_t o0 = s_carry[0], o1 = s_carry[1], t0 = 0, t1 = 0;
+        for (int w = 0; w < 16; ++w) {
+            o0 += (w < wid) ? s_w0[w] : 0u;
+            o1 += (w < wid) ? s_w1[w] : 0u;
+            t0 += s_w0[w];
+            t1 += s_w1[w];
+        }
+        if (i < nblocks) fr.blocksum[i] = make_uint2(o0 + i0 - v.x, o1 + i1 - v.y);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            s_carry[0] += t0;
+            s_carry[1] += t1;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        fr.totals[0] = s_carry[0];
+        fr.totals[1] = s_carry[1];
+    }
+}
+
+// ---------------------------------------------------------------------- emit
+// positions: mains [0,V) in splat order, duplicates [V, V+D) splat-major with the rect
+// walked y-major / x-minor and the main tile skipped (preprocess.glsl:171-188)
+__global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
+                                                 uint32_t *__restrict__ vals) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    int4 rc = make_int4(0, -1, -1, 0);
+    if (i < n) rc = fr.rec[i];
+    const bool has = rc.y >= 0;
+    const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
+    const int tileX = rc.y, tileY = rc.z;
+    uint32_t n_main = 0, n_dup = 0;
+    if (has) {
+        const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+        const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
+        n_main = 1;
+        n_dup = (uint32_t)(rectCount - mainInRect);
+    }
+    uint32_t t0, t1;
+    const uint32_t pm = block_excl_scan256(n_main, s_wave, &t0);
+    const uint32_t pd = block_excl_scan256(n_dup, s_wave, &t1);
+    if (!has) return;
+    const uint2 off = fr.blocksum[blockIdx.x];
+    const uint32_t V = fr.totals[0];
+    const float z = u2f((uint32_t)rc.x);
+    // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
+    const uint32_t mpos = off.x + pm;
+    const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
+    keys[mpos] = f2u((float)tileIndex + z);
+    vals[mpos] = (uint32_t)i;
+    uint32_t d = V + off.y + pd;
+    for (int y = minY; y <= maxY; ++y)
+        for (int x = minX; x <= maxX; ++x) {
+            if (x == tileX && y == tileY) continue;
+            keys[d] = f2u((float)(uint32_t)(y * 16 + x) + z);
+            vals[d] = (uint32_t)i;
+            ++d;
+        }
+}
+
+// ---------------------------------------------------------------------- bins
+// countBins.glsl: bins[int(key)]++ for int(key) in [0,256).  Keys are already sorted, so
+// each thread run-length counts 16 consecutive keys and flushes a run to LDS on change.
+constexpr int kBinItems = 16;
+__global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restrict__ keys, int64_t E,
+                                                       uint32_t *__restrict__ counts) {
+    __shared__ uint32_t s_cnt[256];
+    s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kBinItems;
+    int cur = -1;
+    uint32_t run = 0;
+    if (base < E) {
+        uint32_t kk[kBinItems];
+        if (base + kBinItems <= E) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(keys + base);
+#pragma unroll
+            for (int q = 0; q < kBinItems / 4; ++q) {
+                const uint4 v = p[q];
+                kk[4 * q + 0] = v.x;
+                kk[4 * q + 1] = v.y;
+                kk[4 * q + 2] = v.z;
+                kk[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kBinItems; ++q) kk[q] = (base + q < E) ? keys[base + q] : 0x7f800000u;  // +inf
+        }
+#pragma unroll
+        for (int q = 0; q < kBinItems; ++q) {
+            const int v = f2i(u2f(kk[q]));
+            if (v < 0 || v >= 256) continue;
+            if (v == cur) {
+                ++run;
+            } else {
+                if (run) atomicAdd(&s_cnt[cur], run);
+                cur = v;
+                run = 1;
+            }
+        }
+        if (run) atomicAdd(&s_cnt[cur], run);
+    }
+    __syncthreads();
+    const uint32_t c = s_cnt[threadIdx.x];
+    if (c) atomicAdd(&counts[threadIdx.x], c);
+}
+
+// prefixBins.glsl: inclusive scan of the 256 counts
+__global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict__ counts, uint32_t *__restrict__ bins) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    const uint32_t v = counts[threadIdx.x];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256(v, s_wave, &tot);
+    bins[threadIdx.x] = ex + v;
+}
+
+// ---------------------------------------------------------------------- draw
+// One 256-thread workgroup per 16x16 pixel sub-block of a coarse tile (blocks never
+// straddle coarse tiles, so each pixel blends exactly its own tile's list -- Q18 resolved).
+// The tile's sorted list is streamed in chunks of 256 entries: each lane tests one entry's
+// conservative box against the sub-block, survivors are compacted in order into LDS, then
+// every pixel blends the compacted chunk front to back.  Entries the cull drops would be
+// skipped by draw.glsl:118-126 at every pixel of the sub-block, so results are unchanged.
+template <bool FAST_EXP>
+__global__ __launch_bounds__(kBlock) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
+                                                 const uint32_t *__restrict__ vals, const float2 *__restrict__ m2d,
+                                                 const float4 *__restrict__ conic, const float4 *__restrict__ cullbox,
+                                                 const float4 *__restrict__ colour, uint32_t *__restrict__ out) {
+    __shared__ float4 s_p0[kBlock];  // mx, my, conic.x, conic.y
+    __shared__ float4 s_p1[kBlock];  // conic.z, opacity, r, g
+    __shared__ float s_p2[kBlock];   // b
+    __shared__ uint32_t s_wcnt[kBlock / 64];
+
+    const int tx = blockIdx.x / P.nbx, sbx = blockIdx.x - tx * P.nbx;
+    const int ty = blockIdx.y / P.nby, sby = blockIdx.y - ty * P.nby;
+    const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
+    const int x0 = P.xb[tx] + sbx * 16, y0 = P.yb[ty] + sby * 16;
+    if (x0 >= xe || y0 >= ye) return;  // uniform: sub-block beyond this tile
+    const int x1 = min(x0 + 16, xe), y1 = min(y0 + 16, ye);
+    const int px = x0 + (threadIdx.x & 15), py = y0 + (threadIdx.x >> 4);
+    const bool inside = px < x1 && py < y1;
+    const float fpx = (float)px, fpy = (float)py;
+    const float bx0 = (float)x0, bx1 = (float)(x1 - 1), by0 = (float)y0, by1 = (float)(y1 - 1);
+
+    const int t = ty * 16 + tx;
+    const int start = (t == 0) ? 0 : (int)bins[t - 1];
+    int end = (int)bins[t];
+    if (!P.clean && end > start) {  // Q10: the last 1024-entry chunk is blended whole
+        const int chunks = (end - start + 1023) / 1024;
+        end = min(P.E, start + chunks * 1024);
+    }
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    float cr = 0.f, cg = 0.f, cb = 0.f, ca = 0.f;
+    bool done = !inside;
+
+    for (int base = start; base < end; base += kBlock) {
+        const int j = base + threadIdx.x;
+        bool keep = false;
+        uint32_t v = 0;
+        if (j < end) {
+            v = vals[j];
+            if (P.no_cull) {
+                keep = true;
+            } else {
+                const float4 b = cullbox[v];
+                keep = (b.x <= bx1) && (b.y >= bx0) && (b.z <= by1) && (b.w >= by0);
+            }
+        }
+        const uint64_t bal = __ballot(keep);
+        if (lane == 0) s_wcnt[wid] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t woff = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const uint32_t c = s_wcnt[w];
+            woff += (w < wid) ? c : 0u;
+            total += c;
+        }
+        if (keep) {
+            const uint32_t pos = woff + (uint32_t)__popcll(bal & lanemask_lt());
+            const float2 m = m2d[v];
+            const float4 co = conic[v];
+            const float4 col = colour[v];
+            s_p0[pos] = make_float4(m.x, m.y, co.x, co.y);
+            s_p1[pos] = make_float4(co.z, co.w, col.x, col.y);
+            s_p2[pos] = col.z;
+        }
+        __syncthreads();
+        if (!done) {
+            for (uint32_t k = 0; k < total; ++k) {
+                const float4 a = s_p0[k];
+                const float4 b = s_p1[k];
+                // :111-126
+                const float dx = fpx - a.x, dy = fpy - a.y;
+                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
+                if (power > 0.0f) continue;
+                const float e = FAST_EXP ? __expf(power) : exp_defined(power);
+                const float alpha = fminf(0.99f, e * b.y);
+                if (alpha < 1.0f / 255.0f) continue;
+                // alphaBlend :59-67
+                const float remaining = 1.0f - ca;
+                const float aT = alpha * remaining;
+                cr = cr + b.z * aT;
+                cg = cg + b.w * aT;
+                cb = cb + s_p2[k] * aT;
+                ca = ca + aT;
+                if (ca >= 0.99f) {  // :129-133
+                    done = true;
+                    break;
+                }
+            }
+        }
+        if (__syncthreads_and(done ? 1 : 0)) break;  // every pixel saturated: nothing can change
+    }
+    if (inside) {
+        // :141-142 imageStore(rgba8, col / 255): unorm, round to nearest
+        const float vv[4] = {cr / 255.0f, cg / 255.0f, cb / 255.0f, ca / 255.0f};
+        uint32_t packed = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            float q = vv[c];
+            q = (q != q) ? 0.0f : q;
+            q = q < 0.0f ? 0.0f : (q > 1.0f ? 1.0f : q);
+            packed |= ((uint32_t)floorf(q * 255.0f + 0.5f)) << (8 * c);
+        }
+        out[(size_t)py * P.W + px] = packed;
+    }
+}
+
+}  // namespace
+
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr) {
+    const int nb = (P.n + kBlock - 1) / kBlock;
+    if (nb > 0) hipLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kBlock), 0, s, P, sc, fr);
+}
+
+void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks) {
+    hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, fr, nblocks);
+}
+
+void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals) {
+    const int nb = (n + kBlock - 1) / kBlock;
+    if (nb > 0) hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kBlock), 0, s, n, fr, keys, vals);
+}
+
+void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins) {
+    const int64_t per = (int64_t)kBlock * kBinItems;
+    const int64_t nb = (E + per - 1) / per;
+    if (nb > 0) hipLaunchKernelGGL(k_bins_count, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, E, counts);
+    hipLaunchKernelGGL(k_bins_scan, dim3(1), dim3(kBlock), 0, s, counts, bins);
+}
+
+void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
+                 const FrameDev &fr, const float4 *colour, uint32_t *out) {
+    const dim3 grid(kTiles * P.nbx, kTiles * P.nby);
+    if (P.nbx <= 0 || P.nby <= 0) return;
+    if (fast_exp)
+        hipLaunchKernelGGL(k_draw<true>, grid, dim3(kBlock), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox,
+                           colour, out);
+    else
+        hipLaunchKernelGGL(k_draw<false>, grid, dim3(kBlock), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox,
+                           colour, out);
+}
+
+}  // namespace gs

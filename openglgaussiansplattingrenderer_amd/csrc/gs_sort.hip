@@ -1,0 +1,274 @@
+// gs_sort.hip -- stable LSD radix sort of (uint32 key, uint32 value) pairs on gfx950.
+//
+// Replaces GPURadixSort (src/sort.cpp:139-203) and its shaders generateHistograms.glsl,
+// computePrefixSum.glsl, scan.glsl (8 passes x 4-bit digits, 512 serial threads with
+// indirect key gathers).  Here: 4 passes x 8-bit digits, reduce-then-scan per pass with no
+// inter-workgroup communication inside a launch:
+//   k_upsweep    per 4096-key tile, 256-bin digit histogram -> hist[digit][tile]
+//   k_scan_rows  one workgroup per digit: exclusive scan of hist[digit][*], row totals
+//   k_downsweep  wave64 ballot-match ranking (stable), LDS reorder, coalesced scatter
+// Stability: inside a tile, wave w owns elements [w*1024, (w+1)*1024) in order and ranks them
+// sequentially (item k, then lane), so equal digits keep their input order; tiles are
+// ordered by the digit-major scan.  The result is therefore the unique stable sort -- the
+// one the reference's test (tests/sortTests.cpp:240-243) and the oracle define.
+#include "gs_internal.hpp"
+
+#include <hip/hip_runtime.h>
+
+namespace gs {
+
+namespace {
+
+constexpr int kThreads = 256;                 // 4 waves
+constexpr int kWaves = kThreads / 64;
+constexpr int kItems = 16;                    // keys per lane
+constexpr int kWaveTile = 64 * kItems;        // 1024
+constexpr int kTile = kThreads * kItems;      // 4096
+constexpr int kRadix = 256;
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+
+// mask of the active lanes whose 8-bit digit equals this lane's (8 ballots)
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
+    uint64_t m = active;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// exclusive scan over the 256 threads of a block (one value each)
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) off += (w < wid) ? s_wave[w] : 0u;
+    __syncthreads();
+    return off + inc - v;
+}
+
+__global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
+                                                      uint32_t *__restrict__ hist, uint32_t nb) {
+    __shared__ uint32_t s_cnt[kWaves][kRadix];
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t base = blockIdx.x * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        kk[k] = (idx < n) ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        const bool valid = idx < n;
+        const uint32_t d = (kk[k] >> shift) & 0xffu;
+        const uint64_t m = match_digit(d, __ballot(valid));
+        if (valid && (m & lanemask_lt()) == 0) s_cnt[wid][d] += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    const int d = threadIdx.x;
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tot += s_cnt[w][d];
+    hist[(size_t)d * nb + blockIdx.x] = tot;
+}
+
+// one block per digit: exclusive scan of that digit's per-tile counts, row total
+__global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb,
+                                                    uint32_t *__restrict__ row_total) {
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_carry;
+    uint32_t *row = hist + (size_t)blockIdx.x * nb;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < nb; b += 1024) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = (i < nb) ? row[i] : 0u;
+        const uint32_t inc = wave_incl_scan(v);
+        if (lane == 63) s_w[wid] = inc;
+        __syncthreads();
+        uint32_t off = s_carry, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            off += (w < wid) ? s_w[w] : 0u;
+            tot += s_w[w];
+        }
+        if (i < nb) row[i] = off + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) row_total[blockIdx.x] = s_carry;
+}
+
+__global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                        uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                        uint32_t n, int shift, const uint32_t *__restrict__ hist,
+                                                        uint32_t nb, const uint32_t *__restrict__ row_total) {
+    __shared__ uint32_t s_cnt[kWaves][kRadix];  // running per-wave counts -> per-wave exclusive offsets
+    __shared__ uint32_t s_start[kRadix];        // block-local start of each digit
+    __shared__ int32_t s_gbase[kRadix];         // global position of local slot 0 of each digit
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_keys[kTile];
+    __shared__ uint32_t s_vals[kTile];
+
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t tile0 = blockIdx.x * (uint32_t)kTile;
+    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        kk[k] = (idx < n) ? kin[idx] : 0u;
+        vv[k] = (idx < n) ? vin[idx] : 0u;
+    }
+    uint32_t rank[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        const bool valid = idx < n;
+        const uint32_t d = (kk[k] >> shift) & 0xffu;
+        const uint64_t m = match_digit(d, __ballot(valid));
+        const uint32_t prev = s_cnt[wid][d];
+        rank[k] = prev + (uint32_t)__popcll(m & lanemask_lt());
+        if (valid && (m & lanemask_lt()) == 0) s_cnt[wid][d] = prev + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;  // one thread per digit
+        uint32_t c[kWaves], tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            c[w] = s_cnt[w][d];
+            s_cnt[w][d] = tot;
+            tot += c[w];
+        }
+        const uint32_t start = block_excl_scan(tot, s_wave);
+        const uint32_t gdig = block_excl_scan(row_total[d], s_wave);  // digit base over the whole array
+        s_start[d] = start;
+        s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + blockIdx.x]) - (int32_t)start;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        if (idx < n) {
+            const uint32_t d = (kk[k] >> shift) & 0xffu;
+            const uint32_t pos = s_start[d] + s_cnt[wid][d] + rank[k];
+            s_keys[pos] = kk[k];
+            s_vals[pos] = vv[k];
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = min((uint32_t)kTile, n - tile0);
+    for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) {
+        const uint32_t key = s_keys[i];
+        const uint32_t d = (key >> shift) & 0xffu;
+        const uint32_t o = (uint32_t)(s_gbase[d] + (int32_t)i);
+        kout[o] = key;
+        vout[o] = s_vals[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ keys, const int32_t *__restrict__ order,
+                                                     uint32_t *__restrict__ kout, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) kout[i] = __float_as_uint(keys[order[i]]);
+}
+
+}  // namespace
+
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err) {
+    const size_t nb = (size_t)((n + kTile - 1) / kTile);
+    if ((size_t)n > sc.alt_cap) {
+        if (sc.keys_alt) (void)hipFree(sc.keys_alt);
+        if (sc.vals_alt) (void)hipFree(sc.vals_alt);
+        sc.keys_alt = sc.vals_alt = nullptr;
+        sc.alt_cap = 0;
+        const size_t cap = (size_t)n + (size_t)n / 4 + 4096;
+        if (hipMalloc(&sc.keys_alt, cap * 4) != hipSuccess || hipMalloc(&sc.vals_alt, cap * 4) != hipSuccess) {
+            err = "radix sort: out of device memory";
+            return GS_ERR_NOMEM;
+        }
+        sc.alt_cap = cap;
+    }
+    if (nb * kRadix > sc.hist_cap) {
+        if (sc.hist) (void)hipFree(sc.hist);
+        sc.hist = nullptr;
+        const size_t cap = (nb + nb / 4 + 16) * kRadix;
+        if (hipMalloc(&sc.hist, cap * 4) != hipSuccess) {
+            err = "radix sort: out of device memory";
+            return GS_ERR_NOMEM;
+        }
+        sc.hist_cap = cap;
+    }
+    if (!sc.row_total && hipMalloc(&sc.row_total, kRadix * 4) != hipSuccess) {
+        err = "radix sort: out of device memory";
+        return GS_ERR_NOMEM;
+    }
+    return GS_OK;
+}
+
+void sort_free(SortScratch &sc) {
+    if (sc.keys_alt) (void)hipFree(sc.keys_alt);
+    if (sc.vals_alt) (void)hipFree(sc.vals_alt);
+    if (sc.hist) (void)hipFree(sc.hist);
+    if (sc.row_total) (void)hipFree(sc.row_total);
+    sc = SortScratch{};
+}
+
+int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err) {
+    if (n <= 1) return GS_OK;
+    if (n >= (int64_t)1 << 31) {
+        err = "radix sort: n must be < 2^31";
+        return GS_ERR_INVALID;
+    }
+    int rc = sort_ensure(sc, n, err);
+    if (rc) return rc;
+    const uint32_t nb = (uint32_t)((n + kTile - 1) / kTile);
+    uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 8 * pass;
+        hipLaunchKernelGGL(k_upsweep, dim3(nb), dim3(kThreads), 0, s, kin, (uint32_t)n, shift, sc.hist, nb);
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, sc.row_total);
+        hipLaunchKernelGGL(k_downsweep, dim3(nb), dim3(kThreads), 0, s, kin, vin, kout, vout, (uint32_t)n, shift,
+                           sc.hist, nb, sc.row_total);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+    }
+    // 4 (even) passes: the result is back in (keys, vals)
+    if (hipGetLastError() != hipSuccess) {
+        err = "radix sort: kernel launch failed";
+        return GS_ERR_HIP;
+    }
+    return GS_OK;
+}
+
+void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n) {
+    const int64_t nb = (n + 255) / 256;
+    if (nb > 0) hipLaunchKernelGGL(k_gather_keys, dim3((unsigned)nb), dim3(256), 0, s, keys, order, kout, n);
+}
+
+}  // namespace gs

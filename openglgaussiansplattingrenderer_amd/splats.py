@@ -1,0 +1,444 @@
+"""Host-side mirror of the reference's C++ API for the hot path.
+
+Reference (thomas-chernaik/OpenGLGaussianSplattingRenderer):
+  include/Splats.h:29-124 / src/Splats.cpp   -> class Splats
+  include/sort.h:15-23    / src/sort.cpp     -> GPURadixSort, PadBuffer,
+                                                createAndLinkSortAndHistogramShaders
+  include/Camera.h / src/Camera.cpp          -> class Camera
+  src/utils.cpp:49-63                        -> createRandomNumbersFloat
+
+Same names, argument meaning and error behaviour; the GL objects become device buffers
+owned by a ``Context`` (one per GPU) and every stage runs as HIP kernels through
+``libgsplat_hip.so``.  Matrices are numpy float32 (4,4) arrays indexed like glm,
+``M[c, r] == glm m[c][r]`` (column-major memory).
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+
+import numpy as np
+
+from . import _native as N
+from ._native import check, lib, ptr
+
+
+class Context:
+    """A device + HIP stream (replaces the GL context; one per GPU, not thread-safe)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        check(lib().gs_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().gs_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(lib().gs_sync(self.handle), self.handle)
+
+    def last_kernel_ms(self, kernel: int) -> float:
+        ms = ctypes.c_float()
+        check(lib().gs_last_kernel_ms(self.handle, kernel, ctypes.byref(ms)), self.handle)
+        return ms.value
+
+
+class DeviceBuffer:
+    """A device allocation (stands in for a GL shader-storage buffer object)."""
+
+    def __init__(self, ctx: Context, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().gs_malloc(ctx.handle, self.nbytes, ctypes.byref(p)), ctx.handle)
+        self.ptr = p
+
+    @classmethod
+    def from_array(cls, ctx: Context, a: np.ndarray) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(ctx, a.nbytes)
+        b.upload(a)
+        return b
+
+    def upload(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        if a.nbytes > self.nbytes:
+            raise ValueError("array larger than the buffer")
+        check(lib().gs_memcpy_h2d(self.ctx.handle, self.ptr, ptr(a), a.nbytes), self.ctx.handle)
+
+    def download(self, dtype, count: int) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        if out.nbytes > self.nbytes:
+            raise ValueError("read past the buffer")
+        check(lib().gs_memcpy_d2h(self.ctx.handle, ptr(out), self.ptr, out.nbytes), self.ctx.handle)
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().gs_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# --------------------------------------------------------------------- sort API
+def createAndLinkSortAndHistogramShaders():
+    """src/sort.cpp:15-124.  Nothing to compile at run time (kernels are built ahead of
+    time for gfx950); returns placeholder program handles (histogram, sort, sum)."""
+    print("compiling sorting shaders")
+    print("compiled and linked sorting shaders")
+    return 1, 2, 3
+
+
+def PadBuffer(size: int, unitWidth: int) -> int:
+    """src/sort.cpp:127-137"""
+    return int(lib().gs_pad_buffer(int(size), int(unitWidth)))
+
+
+def GPURadixSort(histogramProgram, prefixSumProgram, sortProgram, intermediateBuffer, orderBuffer: DeviceBuffer,
+                 histogramBuffer, size: int, workGroupCount: int, workGroupSize: int, buffer: DeviceBuffer):
+    """src/sort.cpp:139-203: stable argsort of the float keys in ``buffer`` by their bits.
+
+    ``orderBuffer`` (int32[size]) is read as the initial order and receives the sorted
+    order; the keys are not moved.  Program handles, ``intermediateBuffer``,
+    ``histogramBuffer`` and the workgroup shape are accepted for signature parity; the
+    HIP sort keeps its own scratch in the context.
+    """
+    number_of_sections = workGroupCount * workGroupSize
+    if number_of_sections <= 0:
+        print(f"Size must be a multiple of {number_of_sections}", file=sys.stderr)
+        return
+    ctx = orderBuffer.ctx
+    check(lib().gs_argsort_f32(ctx.handle, buffer.ptr, orderBuffer.ptr, int(size)), ctx.handle)
+
+
+def sort_pairs(ctx: Context, keys: DeviceBuffer, vals: DeviceBuffer, n: int):
+    """Stable in-place sort of (uint32 key, uint32 value) pairs by key."""
+    check(lib().gs_sort_pairs_u32(ctx.handle, keys.ptr, vals.ptr, int(n)), ctx.handle)
+
+
+# ------------------------------------------------------------------- test RNG
+def createRandomNumbersFloat(size: int) -> np.ndarray:
+    """src/utils.cpp:49-63 -- srand(20), glibc rand(): rand()%255 + rand()/RAND_MAX + 0.5"""
+    if size < 1:
+        print("Error: size must be greater than 0", file=sys.stderr)
+        return np.zeros(0, np.float32)
+    libc = ctypes.CDLL("libc.so.6")
+    libc.rand.restype = ctypes.c_int
+    libc.srand(20)
+    raw = np.fromiter((libc.rand() for _ in range(2 * size)), dtype=np.int64, count=2 * size)
+    random = (raw[0::2] % 255).astype(np.float32)
+    frac = raw[1::2].astype(np.float32) / np.float32(2147483647)
+    return (frac + random) + np.float32(0.5)
+
+
+# --------------------------------------------------------------------- camera
+class Camera:
+    """src/Camera.cpp restatement (uniform generator).  Keeps the reference's quirks:
+    tan() of degrees in getTanFovx/y (Q1) and focal_x from fovy (Q3)."""
+
+    def __init__(self, x: float = 0.0, y: float = 0.0, z: float = 0.0, *, width: int = 1024, height: int = 512,
+                 near: float | None = None):
+        self.position = np.array([x, y, z], np.float32)
+        self.rotation = np.zeros(3, np.float32)
+        self.fovy = 60.0
+        # Camera() uses near 0.0001, Camera(x,y,z) uses 0.1 (src/Camera.cpp:13,25)
+        self.near = 0.1 if near is None else near
+        self.far = 10000.0
+        self.width, self.height = int(width), int(height)
+
+    def _c(self) -> N.gs_camera:
+        c = N.gs_camera()
+        for k in range(3):
+            c.position[k] = float(self.position[k])
+            c.rotation[k] = float(self.rotation[k])
+        c.fovy, c.near_plane, c.far_plane = self.fovy, self.near, self.far
+        c.width, c.height = self.width, self.height
+        return c
+
+    def _update(self):
+        view = np.zeros(16, np.float32)
+        proj = np.zeros(16, np.float32)
+        fx, fy, tx, ty = (ctypes.c_float() for _ in range(4))
+        check(lib().gs_camera_update(ctypes.byref(self._c()), ptr(view), ptr(proj), ctypes.byref(fx), ctypes.byref(fy),
+                                     ctypes.byref(tx), ctypes.byref(ty)))
+        return view.reshape(4, 4), proj.reshape(4, 4), fx.value, fy.value, tx.value, ty.value
+
+    def update(self):
+        pass  # state is recomputed on demand
+
+    def setWidthHeight(self, width: int, height: int):
+        self.width, self.height = int(width), int(height)
+
+    def getWidth(self) -> int:
+        return self.width
+
+    def getHeight(self) -> int:
+        return self.height
+
+    def getViewMatrix(self) -> np.ndarray:
+        return self._update()[0]
+
+    def getProjectionMatrix(self) -> np.ndarray:
+        return self._update()[1]
+
+    def getFocalX(self) -> float:
+        return self._update()[2]
+
+    def getFocalY(self) -> float:
+        return self._update()[3]
+
+    def getTanFovx(self) -> float:
+        return self._update()[4]
+
+    def getTanFovy(self) -> float:
+        return self._update()[5]
+
+    def rotateRight(self, angle: float):
+        self.rotation[1] = np.float32(self.rotation[1] + np.float32(angle))
+
+    def rotateLeft(self, angle: float):
+        self.rotateRight(-angle)
+
+    def rotateUp(self, angle: float):
+        self.rotation[0] = np.float32(self.rotation[0] + np.float32(angle))
+
+    def rotateDown(self, angle: float):
+        self.rotateUp(-angle)
+
+    def moveForward(self, distance: float):
+        v = self.getViewMatrix()  # upper-left 3x3 of view == rotationMatrix (view = R * T)
+        d = np.float32(distance)
+        self.position = (self.position + np.array([v[0, 2] * d, v[1, 2] * d, v[2, 2] * d], np.float32)).astype(np.float32)
+
+    def moveBackward(self, distance: float):
+        self.moveForward(-distance)
+
+    def moveLeft(self, distance: float):
+        v = self.getViewMatrix()
+        d = np.float32(distance)
+        self.position = (self.position + np.array([v[0, 0] * d, v[1, 0] * d, v[2, 0] * d], np.float32)).astype(np.float32)
+
+    def moveRight(self, distance: float):
+        self.moveLeft(-distance)
+
+    def moveUp(self, distance: float):
+        self.position = (self.position + np.array([0, distance, 0], np.float32)).astype(np.float32)
+
+    def moveDown(self, distance: float):
+        self.moveUp(-distance)
+
+    def uniforms(self) -> N.gs_uniforms:
+        """The gpuRender arguments exactly as main.cpp:62-64 passes them (tan x/y swapped, Q2)."""
+        u = N.gs_uniforms()
+        check(lib().gs_camera_uniforms(ctypes.byref(self._c()), ctypes.byref(u)))
+        return u
+
+
+def main_camera(width: int = 1024, height: int = 512) -> Camera:
+    """main.cpp:40-45 pose: Camera(5, 0.5, -4); rotateDown(20); rotateRight(40)."""
+    cam = Camera(5.0, 0.5, -4.0)
+    cam.rotateDown(20.0)
+    cam.rotateRight(40.0)
+    cam.setWidthHeight(width, height)
+    return cam
+
+
+def make_uniforms(view, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vp) -> N.gs_uniforms:
+    u = N.gs_uniforms()
+    v = np.ascontiguousarray(view, np.float32).reshape(16)
+    p = np.ascontiguousarray(vp, np.float32).reshape(16)
+    for k in range(16):
+        u.view[k] = float(v[k])
+        u.vp[k] = float(p[k])
+    u.width, u.height = int(width), int(height)
+    u.focal_x, u.focal_y = float(focal_x), float(focal_y)
+    u.tan_fov_x, u.tan_fov_y = float(tan_fov_x), float(tan_fov_y)
+    return u
+
+
+# ------------------------------------------------------------- loader helpers
+def load_ply(filePath: str):
+    """src/Splats.cpp:174-344 through the library's C++ loader.
+    Returns means3D (N,4), colours (N,4), opacities (N,), scales (N,3), rotations (N,4)."""
+    n = ctypes.c_int()
+    check(lib().gs_ply_count(filePath.encode(), ctypes.byref(n)))
+    N_ = n.value
+    means = np.zeros((N_, 4), np.float32)
+    cols = np.zeros((N_, 4), np.float32)
+    op = np.zeros(N_, np.float32)
+    sc = np.zeros((N_, 3), np.float32)
+    rot = np.zeros((N_, 4), np.float32)
+    check(lib().gs_ply_load(filePath.encode(), N_, ptr(means), ptr(cols), ptr(op), ptr(sc), ptr(rot)))
+    return means, cols, op, sc, rot
+
+
+def save_ply(path: str, means, rotations, scales, opacities, colours):
+    """tests/plyFileGenerator.py:155-249 byte layout, via the library's C++ writer."""
+    m = np.ascontiguousarray(means, np.float32).reshape(-1, 3)
+    r = np.ascontiguousarray(rotations, np.float32).reshape(-1, 4)
+    s = np.ascontiguousarray(scales, np.float32).reshape(-1, 3)
+    o = np.ascontiguousarray(opacities, np.float32).reshape(-1)
+    c = np.ascontiguousarray(colours, np.float32).reshape(-1, 3)
+    check(lib().gs_ply_write(path.encode(), len(m), ptr(m), ptr(r), ptr(s), ptr(o), ptr(c)))
+
+
+def activate(f_dc, opacity_logit, log_scale, rot_raw):
+    """the loader's activations on raw records (same arithmetic as loadSplats)"""
+    f = np.ascontiguousarray(f_dc, np.float32).reshape(-1, 3)
+    n = len(f)
+    o = np.ascontiguousarray(opacity_logit, np.float32).reshape(-1)
+    s = np.ascontiguousarray(log_scale, np.float32).reshape(-1, 3)
+    r = np.ascontiguousarray(rot_raw, np.float32).reshape(-1, 4)
+    cols = np.zeros((n, 4), np.float32)
+    op = np.zeros(n, np.float32)
+    sc = np.zeros((n, 3), np.float32)
+    rot = np.zeros((n, 4), np.float32)
+    check(lib().gs_activate(n, ptr(f), ptr(o), ptr(s), ptr(r), ptr(cols), ptr(op), ptr(sc), ptr(rot)))
+    return cols, op, sc, rot
+
+
+def covariance3d(scales, rotations) -> np.ndarray:
+    """src/Splats.cpp:414-479 -> flat float32[6N]"""
+    s = np.ascontiguousarray(scales, np.float32).reshape(-1, 3)
+    r = np.ascontiguousarray(rotations, np.float32).reshape(-1, 4)
+    out = np.zeros(6 * len(s), np.float32)
+    check(lib().gs_covariance3d(len(s), ptr(s), ptr(r), ptr(out)))
+    return out
+
+
+# --------------------------------------------------------------------- Splats
+class Splats:
+    """include/Splats.h:29-124.  ``Splats(path, width, height)`` loads the ply, computes the
+    3D covariances on the host and uploads the scene; ``gpuRender`` runs the frame as HIP
+    kernels.  ``flags`` selects ref (default: the reference's deterministic quirks kept) or
+    GS_FLAG_CLEAN, and the blend's exp (bit-exact polynomial or GS_FLAG_FAST_EXP)."""
+
+    def __init__(self, filePath: str | None, width: int, height: int, *, ctx: Context | None = None,
+                 device: int = 0, flags: int = 0, arrays=None):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.flags = int(flags)
+        print("setting up splats")
+        if arrays is None:
+            self.loadSplats(filePath)
+        else:
+            self.means3D, self.colours, self.opacities, self.scales, self.rotations = arrays
+            self.numSplats = len(self.means3D)
+        self.sphericalHarmonics = np.zeros(0, np.float32)  # never filled (include/Splats.h:59)
+        self.numDuplicates = 0
+        self.computeCovarianceMatrices()
+        self._scene = None
+        self.loadToGPU(width, height)
+        print("finished setting up splats")
+
+    @classmethod
+    def from_raw(cls, means3, f_dc, opacity_logit, log_scale, rot_raw, width, height, **kw) -> "Splats":
+        """Scene from raw (pre-activation) ply fields -- what loadSplats would read from a file."""
+        cols, op, sc, rot = activate(f_dc, opacity_logit, log_scale, rot_raw)
+        m = np.ascontiguousarray(means3, np.float32).reshape(-1, 3)
+        means4 = np.concatenate([m, np.ones((len(m), 1), np.float32)], axis=1)
+        return cls(None, width, height, arrays=(means4, cols, op, sc, rot), **kw)
+
+    # src/Splats.cpp:174-344
+    def loadSplats(self, filePath: str):
+        print("Loading splats from file")
+        self.means3D, self.colours, self.opacities, self.scales, self.rotations = load_ply(filePath)
+        self.numSplats = len(self.means3D)
+        print(f"num splats: {self.numSplats}")
+        print("Finished loading splats from file")
+
+    # src/Splats.cpp:414-438
+    def computeCovarianceMatrices(self):
+        self.covarianceMatrices = covariance3d(self.scales, self.rotations)
+
+    def loadShaders(self):
+        """src/Splats.cpp:156-172 -- kernels are compiled ahead of time; nothing to do."""
+
+    # src/Splats.cpp:61-154
+    def loadToGPU(self, width: int, height: int):
+        if self._scene is not None:
+            lib().gs_scene_destroy(self._scene)
+            self._scene = None
+        h = ctypes.c_void_p()
+        check(lib().gs_scene_create(self.ctx.handle, self.numSplats, ptr(np.ascontiguousarray(self.means3D, np.float32)),
+                                    ptr(self.covarianceMatrices), ptr(np.ascontiguousarray(self.opacities, np.float32)),
+                                    ptr(np.ascontiguousarray(self.colours, np.float32)), ctypes.byref(h)), self.ctx.handle)
+        self._scene = h
+        self.width, self.height = int(width), int(height)
+        self._texture = DeviceBuffer(self.ctx, self.width * self.height * 4)
+        self.stats = N.gs_frame_stats()
+
+    def __del__(self):
+        try:
+            if self._scene is not None:
+                lib().gs_scene_destroy(self._scene)
+                self._scene = None
+        except Exception:
+            pass
+
+    # src/Splats.cpp:542-585
+    def preprocess(self, viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix):
+        u = make_uniforms(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix)
+        self._preprocess_u(u)
+
+    def _preprocess_u(self, u: N.gs_uniforms):
+        check(lib().gs_preprocess(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, ctypes.byref(self.stats)),
+              self.ctx.handle)
+        self.numDuplicates = int(self.stats.duplicates)
+
+    # src/Splats.cpp:346-354
+    def sort(self):
+        check(lib().gs_sort(self.ctx.handle), self.ctx.handle)
+
+    # src/Splats.cpp:481-512
+    def computeBins(self):
+        check(lib().gs_compute_bins(self.ctx.handle), self.ctx.handle)
+
+    # src/Splats.cpp:356-381
+    def draw(self, width: int, height: int, tileWidth: float, tileHeight: float):
+        if width * height * 4 > self._texture.nbytes:
+            self._texture = DeviceBuffer(self.ctx, width * height * 4)
+        self.width, self.height = int(width), int(height)
+        check(lib().gs_draw(self.ctx.handle, self._scene, int(width), int(height), float(tileWidth), float(tileHeight),
+                            self.flags, self._texture.ptr, 1), self.ctx.handle)
+
+    # src/Splats.cpp:587-597
+    def gpuRender(self, viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix):
+        u = make_uniforms(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix)
+        self.render_uniforms(u)
+
+    def render_uniforms(self, u: N.gs_uniforms):
+        if u.width * u.height * 4 > self._texture.nbytes:
+            self._texture = DeviceBuffer(self.ctx, u.width * u.height * 4)
+        self.width, self.height = int(u.width), int(u.height)
+        check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, self._texture.ptr, 1,
+                              ctypes.byref(self.stats)), self.ctx.handle)
+        self.numDuplicates = int(self.stats.duplicates)
+
+    def texture(self) -> np.ndarray:
+        """RGBA8 image (H, W, 4); row 0 = GL row 0 (bottom of the screen)."""
+        return self._texture.download(np.uint8, self.width * self.height * 4).reshape(self.height, self.width, 4)
+
+    def display(self) -> np.ndarray:
+        """src/Splats.cpp:383-412 presents the texture with a y-flip (renderTexture.vert:11);
+        headless: returns the top-down image."""
+        return self.texture()[::-1]
+
+    # frame-state readback (parity tests)
+    def read(self, what: int, count: int, dtype=np.uint32) -> np.ndarray:
+        out = np.empty(count, dtype=dtype)
+        check(lib().gs_frame_read(self.ctx.handle, what, ptr(out), count), self.ctx.handle)
+        return out

@@ -1,0 +1,245 @@
+"""CPU tests: the oracle pinned against the reference's own known answers and an independent
+float64 restatement, plus the committed golden fixtures (mirrors tests/sortTests.cpp and
+tests/plyParseTests.cpp of the reference)."""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests import ref_f64
+
+SORT_N = 32 * 16 * 10000 - 7  # tests/sortTests.cpp:181
+# BASELINE.md section 4 (FNV-1a-64, one 32-bit word per step)
+GOLD_EQ_PAIRS = 480_979
+GOLD_FIRST3 = [0x423CF5E2, 0x40384EF2, 0x42CBC7DD]
+GOLD_FNV_SORTED_KEYS = 0xF7C786D96C9BBF6A
+GOLD_FNV_PERMUTATION = 0x127693EABFDBBEA9
+
+
+def test_sort_known_answer(oracle):
+    """SortTest.SortTest (tests/sortTests.cpp:127-253) on the oracle's restatement of
+    GPURadixSort: std::sort key sequence and the golden hashes of the stable permutation."""
+    keys = oracle.gen_sort_keys(SORT_N)
+    bits = keys.view(np.uint32)
+    assert [int(b) for b in bits[:3]] == GOLD_FIRST3
+    assert keys.min() >= 0.5 and keys.max() <= 255.5
+    order = oracle.argsort_f32(keys)
+    s = keys[order]
+    assert np.all(s[1:] >= s[:-1])                            # sortTests.cpp:241
+    assert np.array_equal(s, np.sort(keys))                   # sortTests.cpp:242
+    assert int(np.sum(s[1:] == s[:-1])) == GOLD_EQ_PAIRS
+    assert oracle.fnv1a64_words(bits[order]) == GOLD_FNV_SORTED_KEYS
+    assert oracle.fnv1a64_words(order) == GOLD_FNV_PERMUTATION
+    assert np.array_equal(order, np.argsort(keys, kind="stable"))
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 511, 512, 513, 1000, 10_000, 20_000, 300_000])
+def test_sort_sizes_stable(oracle, n):
+    """Q15: the reference mis-sorts n <~ 262k (stale section histograms); the restatement
+    sorts stably at every n, including the sizes the reference gets wrong."""
+    rng = np.random.default_rng(n)
+    keys = (rng.integers(0, 64, n) + rng.integers(0, 4, n) * 0.25).astype(np.float32)  # many ties
+    order = oracle.argsort_f32(keys) if n else np.zeros(0, np.int32)
+    assert np.array_equal(order, np.argsort(keys, kind="stable"))
+
+
+def test_sort_negative_and_special_keys(oracle):
+    """floatBitsToUint order: negatives sort after all non-negatives (Q6)."""
+    keys = np.array([3.5, -0.25, 0.0, -0.0, 255.9, 1e6, -3.0, 17.25, 0.0], np.float32)
+    order = oracle.argsort_f32(keys)
+    assert np.array_equal(order, np.argsort(keys.view(np.uint32), kind="stable"))
+
+
+def test_sort_pairs_matches_argsort(oracle):
+    rng = np.random.default_rng(3)
+    k = rng.integers(0, 2**32, 50_000, dtype=np.uint64).astype(np.uint32)
+    k[::7] = k[3]
+    v = np.arange(len(k), dtype=np.uint32)
+    ks, vs = oracle.sort_pairs(k, v)
+    o = np.argsort(k, kind="stable")
+    assert np.array_equal(ks, k[o]) and np.array_equal(vs, v[o])
+
+
+def test_ply_single_item(oracle, golden_dir):
+    """SplatsTest.LoadSimplePly (tests/plyParseTests.cpp:105-109) + decoded values."""
+    means, cols, op, sc, rot = oracle.ply_load(os.path.join(golden_dir, "testSingleItem.ply"))
+    assert len(means) == 1
+    assert np.array_equal(means[0], np.float32([0, 0, 0, 1]))
+    c0 = np.float32(0.28209479177387814)
+    assert np.array_equal(cols[0, :3], np.full(3, (np.float32(0.5) + c0 * np.float32(1)) * np.float32(255), np.float32))
+    assert abs(op[0] - 0.9) < 1e-6
+    assert np.allclose(sc[0], [1.0, 0.5, 0.5], atol=1e-6)
+    assert np.array_equal(rot[0], np.float32([0, 0, 0, 1]))
+
+
+def test_ply_loader_product_matches_oracle(oracle, golden_dir):
+    """The library's C++ loader == the oracle's restatement, bit for bit (C2 scene)."""
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c2.ply")
+        g.save_ply(p, *c2_scene())
+        a = g.load_ply(p)
+        b = oracle.ply_load(p)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
+def test_ply_writer_regenerates_fixture(golden_dir, tmp_path):
+    """save_ply (tests/plyFileGenerator.py:155-249) byte layout: the writer regenerates the
+    reference's testSingleItem.ply byte for byte from its decoded values."""
+    import openglgaussiansplattingrenderer_amd as g
+    p = str(tmp_path / "t.ply")
+    g.save_ply(p, np.zeros((1, 3)), np.float32([[0, 0, 0, 1]]), np.float32([[1, 0.5, 0.5]]), np.float32([0.9]),
+               np.float32([[1, 1, 1]]))
+    assert open(p, "rb").read() == open(os.path.join(golden_dir, "testSingleItem.ply"), "rb").read()
+
+
+def test_ply_bad_files(oracle, tmp_path):
+    import openglgaussiansplattingrenderer_amd as g
+    with pytest.raises(g.GsError):
+        g.load_ply(str(tmp_path / "missing.ply"))
+    p = tmp_path / "trunc.ply"
+    data = open(os.path.join(os.path.dirname(__file__), "golden", "testSingleItem.ply"), "rb").read()
+    p.write_bytes(data[:-8])
+    with pytest.raises(g.GsError):
+        g.load_ply(str(p))
+    p.write_bytes(data + b"\x00")  # trailing byte: not at EOF (src/Splats.cpp:333-340)
+    with pytest.raises(g.GsError):
+        g.load_ply(str(p))
+
+
+def test_covariance_product_matches_oracle_and_f64(oracle):
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    means, rot, sc, op, col = c2_scene(2000)
+    a = g.covariance3d(sc, rot)
+    b = oracle.cov3d(sc, rot)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # independent check: Sigma = R S^2 R^T with R from the quaternion (r, x, y, z)
+    r, x, y, z = [rot[:, k].astype(np.float64) for k in range(4)]
+    R = np.stack([np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], -1),
+                  np.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], -1),
+                  np.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1)], 1)
+    S2 = np.zeros((len(sc), 3, 3))
+    for k in range(3):
+        S2[:, k, k] = sc[:, k].astype(np.float64) ** 2
+    Sig = R @ S2 @ np.transpose(R, (0, 2, 1))
+    ref = Sig[:, [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]]
+    got = b.reshape(-1, 6).astype(np.float64)
+    scale = np.abs(ref).max(axis=1, keepdims=True)
+    assert np.max(np.abs(got - ref) / scale) < 1e-5
+
+
+def test_camera_matches_survey_numbers():
+    """SURVEY 8.1 camera table (main.cpp:40-45 pose)."""
+    import openglgaussiansplattingrenderer_amd as g
+    u = g.main_camera(256, 256).uniforms()
+    assert abs(u.focal_x - 221.70) < 0.01 and abs(u.focal_y - 221.70) < 0.01
+    assert abs(u.tan_fov_x - -6.4053) < 1e-3 and abs(u.tan_fov_y - -6.4053) < 1e-3
+    VP = ref_f64.glm(u.vp[:])
+    p = VP @ np.array([0, 0, 0, 1.0])
+    p /= p[3]
+    assert abs((p[2] + 1) / 2 - 0.983537) < 1e-5
+    assert abs((p[0] + 1) / 2 * 256 - 174.0) < 0.05 and abs((p[1] + 1) / 2 * 256 - 66.7) < 0.05
+    u = g.main_camera(1920, 1080).uniforms()
+    assert abs(u.focal_x - 1662.77) < 0.01 and abs(u.focal_y - 935.31) < 0.01
+    assert abs(u.tan_fov_x - -6.4053) < 1e-3 and abs(u.tan_fov_y - -11.3873) < 1e-3
+
+
+def test_pad_buffer():
+    import openglgaussiansplattingrenderer_amd as g
+    assert g.PadBuffer(SORT_N, 512) == 7
+    assert g.PadBuffer(1024, 512) == 0
+    assert g.PadBuffer(1, 512) == 511
+
+
+def test_random_numbers_match_reference_generator(oracle):
+    import openglgaussiansplattingrenderer_amd as g
+    a = g.createRandomNumbersFloat(5000)
+    b = oracle.gen_sort_keys(5000)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _load_c2():
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "c2.ply")
+        g.save_ply(p, *c2_scene())
+        return g.load_ply(p)
+
+
+def test_preprocess_oracle_vs_f64():
+    """Oracle preprocess (float32, glm order) vs the independent float64 restatement."""
+    from oracle import oracle as O
+    import openglgaussiansplattingrenderer_amd as g
+    means, cols, op, sc, rot = _load_c2()
+    cov = O.cov3d(sc, rot)
+    u = g.main_camera(512, 512).uniforms()
+    r = O.render(means, cov, op, cols, u, flags=0, draw=False)
+    f = ref_f64.preprocess(means, cov, op, u)
+    vis = r["counts"][0::2] == 1
+    assert np.array_equal(vis, ~f["culled"] & (f["det"] != 0))
+    m2 = r["means2d"].reshape(-1, 2)
+    assert np.max(np.abs(m2[vis, 0] - f["sx"][vis])) < 2e-3
+    assert np.max(np.abs(m2[vis, 1] - f["sy"][vis])) < 2e-3
+    co = r["conics"].reshape(-1, 4)[vis, :3].astype(np.float64)
+    cf = f["conic"][vis]
+    rel = np.abs(co - cf) / np.maximum(np.abs(cf).max(axis=1, keepdims=True), 1e-30)
+    assert np.quantile(rel, 0.999) < 1e-4
+    assert np.allclose(r["z01"][vis], f["z01"][vis], atol=1e-6)
+    # main tile: int(p / tile) -- agrees except where p sits within rounding of a boundary
+    tw = float(512 // 16)
+    tx = np.floor(f["sx"][vis] / tw).astype(int)
+    assert np.mean(r["tilexy"][0::2][vis] == tx) > 0.999
+
+
+def test_draw_oracle_vs_f64():
+    """Oracle blend vs a float64 numpy blend on a small frame: all covered pixels within
+    +-2 LSB, >= 99.5% within +-1 (only exp / float32 rounding differ)."""
+    from oracle import oracle as O
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    means, rot, sc, op, col = c2_scene(600, seed=7)
+    cols, opa, scl, rt = g.activate(col, np.log(op / (1 - op)), np.log(sc), rot)
+    means4 = np.concatenate([means, np.ones((len(means), 1), np.float32)], 1)
+    cov = O.cov3d(scl, rt)
+    for W, H, flags in ((96, 64, 1), (64, 64, 0)):
+        u = g.main_camera(W, H).uniforms()
+        r = O.render(means4, cov, opa, cols, u, flags=flags)
+        ref = ref_f64.draw(W, H, r["vals"], r["bins"], r["means2d"], r["conics"], cols, clean=bool(flags), E=r["E"])
+        d = np.abs(r["image"].astype(int) - ref.astype(int))
+        assert d.max() <= 2 and np.mean(d <= 1) >= 0.995, (W, H, d.max())
+
+
+def test_expf_accuracy(oracle):
+    x = np.linspace(-80, 0, 20001).astype(np.float32)
+    got = np.array([oracle.expf(float(v)) for v in x], np.float64)
+    ref = np.exp(x.astype(np.float64))
+    rel = np.abs(got - ref) / ref
+    assert rel.max() < 4e-7  # a few float32 ulp
+    assert oracle.expf(0.0) == 1.0 and oracle.expf(-100.0) == 0.0
+
+
+@pytest.mark.parametrize("name", ["c1", "c2"])
+def test_golden_fixtures_reproduce(oracle, golden_dir, name):
+    """The oracle reproduces the committed fixtures exactly (drift guard for the fixtures,
+    the scene generator and the oracle itself)."""
+    import openglgaussiansplattingrenderer_amd as g
+    from tests.golden.make_golden import U, scene_c1, scene_c2, scene_hash
+    z = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
+    with tempfile.TemporaryDirectory() as td:
+        scene = scene_c1() if name == "c1" else scene_c2(td)
+    assert scene_hash(*scene) == int(z["scene_hash"])
+    means, cols, op, sc, rot = scene
+    u = U(z["uniforms"])
+    u2 = g.main_camera(u.width, u.height).uniforms()
+    assert list(u2.vp) == [float(np.float32(x)) for x in u.vp]
+    cov = oracle.cov3d(sc, rot)
+    for mode, flags in (("ref", 0), ("clean", 1)):
+        r = oracle.render(means, cov, op, cols, u, flags=flags)
+        assert np.array_equal([r["V"], r["D"], r["E"]], z[f"{mode}_VDE"])
+        for k in ("keys", "vals", "bins", "means2d", "conics", "image"):
+            assert np.array_equal(r[k], z[f"{mode}_{k}"]), (mode, k)
