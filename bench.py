@@ -1,0 +1,271 @@
+#!/usr/bin/env python
+"""bench.py -- frames/s at 1920x1080 on the bicycle-sized scene (+ radix-sort Gkeys/s), with
+the HBM roofline of the dominant kernel and a bounded CPU-oracle baseline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2] [--clean] [--fast-exp]
+
+One frame = one step of the hot path (preprocess -> sort -> bins -> blend) over the
+resident scene (BASELINE.json configs[2]: 6,131,954 splats at 1920x1080; the real bicycle
+point_cloud.ply when $GS_BICYCLE_PLY names it, else the seeded synthetic stand-in).
+Multi-GPU = replicas: rank k renders its own view (main.cpp pose + rotateRight(45 deg * k))
+of its own copy of the scene; no collective on the data path.  Barrier +
+device sync around exactly K timed frames; max time over ranks; rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "frames/s @1080p (bicycle ~6M splats) + radix-sort Gkeys/s; %HBM peak"
+SORT_N = 32 * 16 * 10000 - 7  # tests/sortTests.cpp:181
+
+CONFIGS = {
+    "c3": dict(W=1920, H=1080, desc="C3: bicycle-sized scene, 1920x1080, 1 view per GPU"),
+    "c4": dict(W=3840, H=2160, desc="C4: bicycle-sized scene, 3840x2160, 1 view per GPU"),
+    "c2": dict(W=512, H=512, desc="C2: 10k synthetic splats, 512x512"),
+}
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # timing / barrier plumbing only: gloo on the host (there is no data-path collective)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier(pg):
+    if pg is not None:
+        pg.barrier()
+
+
+def max_over_ranks(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(pg, x: float) -> float:
+    if pg is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64)
+    pg.all_reduce(t, op=pg.ReduceOp.SUM)
+    return float(t.item())
+
+
+def load_scene(cfg: str, W: int, H: int, ctx, flags: int):
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import BICYCLE_N, bicycle_standin_raw, c2_scene
+    if cfg == "c2":
+        means, rot, sc, op, col = c2_scene()
+        sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx, flags=flags)
+        return sp, "synthetic (C2 generator, seed 20240101)"
+    path = os.environ.get("GS_BICYCLE_PLY")
+    if path and os.path.exists(path):
+        return g.Splats(path, W, H, ctx=ctx, flags=flags), f"bicycle point_cloud.ply ({path})"
+    raw = bicycle_standin_raw(BICYCLE_N)
+    return g.Splats.from_raw(*raw, W, H, ctx=ctx, flags=flags), \
+        f"synthetic stand-in for bicycle ({BICYCLE_N:,} splats, seeded; no checkpoint available)"
+
+
+def camera_for_rank(W: int, H: int, rank: int):
+    import openglgaussiansplattingrenderer_amd as g
+    cam = g.main_camera(W, H)
+    cam.rotateRight(45.0 * rank)  # C5: pose k = main pose + rotateRight(45 deg * k)
+    return cam
+
+
+def sort_bench(ctx, reps: int = 50, warm: int = 5):
+    """radix-sort Gkeys/s on the sortTests input (5,119,993 srand(20) keys), GPURadixSort
+    semantics (argsort of float keys); median of `reps` hipEvent-timed sorts."""
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.splats import createRandomNumbersFloat
+    keys = createRandomNumbersFloat(SORT_N)
+    iota = np.arange(SORT_N, dtype=np.int32)
+    kb = g.DeviceBuffer.from_array(ctx, keys)
+    ob = g.DeviceBuffer.from_array(ctx, iota)
+    ms = []
+    for i in range(warm + reps):
+        ob.upload(iota)
+        g.GPURadixSort(1, 3, 2, None, ob, None, SORT_N, 16, 32, kb)
+        t = ctx.last_kernel_ms(g.GS_KERNEL_SORT)
+        if i >= warm:
+            ms.append(t)
+    out = ob.download(np.int32, SORT_N)
+    s = keys[out]
+    ok = bool(np.all(s[1:] >= s[:-1]))
+    # pair sort of the same keys (32-bit key + 32-bit payload): the renderer's sort
+    kbits = keys.view(np.uint32)
+    k2 = g.DeviceBuffer.from_array(ctx, kbits)
+    v2 = g.DeviceBuffer.from_array(ctx, iota)
+    ms_pairs = []
+    for i in range(warm + reps):
+        k2.upload(kbits)
+        v2.upload(iota)
+        g.sort_pairs(ctx, k2, v2, SORT_N)
+        t = ctx.last_kernel_ms(g.GS_KERNEL_SORT)
+        if i >= warm:
+            ms_pairs.append(t)
+    med = float(np.median(ms))
+    medp = float(np.median(ms_pairs))
+    return dict(n=SORT_N, ms_argsort=med, gkeys_per_s=SORT_N / med / 1e6, ms_pairs=medp,
+                gkeys_per_s_pairs=SORT_N / medp / 1e6,
+                hbm_frac_pairs=68.0 * SORT_N / (medp * 1e-3) / 1e9 / HBM_PEAK_GBS, sorted_ok=ok)
+
+
+def cpu_baseline(sp, u, flags, budget_s: float = 20.0):
+    """CPU oracle on the host cores, bounded: full preprocess + emit + sort + bins of the
+    same frame, blend on every row_step-th pixel row (time scaled by row_step)."""
+    from oracle import oracle as O
+    O.build()
+    probe = O.time_frame(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags,
+                         row_step=max(1, u.height // 4))
+    fixed = probe["preprocess_s"] + probe["sort_s"] + probe["bins_s"]
+    per_row = probe["draw_sample_s"] / max(1, len(range(0, u.height, probe["row_step"])))
+    rows = int(max(1, min(u.height, (budget_s - fixed) / max(per_row, 1e-6))))
+    step = max(1, u.height // rows)
+    r = O.time_frame(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags, row_step=step)
+    return dict(value=1.0 / r["frame_est_s"], unit="frames/s", cores=int(r["threads"]), kind="port",
+                sample=(f"oracle/gs_oracle.c (OpenMP, {r['threads']} threads) on the same frame: full preprocess+emit "
+                        f"({r['preprocess_s']:.2f}s), stable sort ({r['sort_s']:.2f}s), bins; blend of every "
+                        f"{step}th pixel row ({r['draw_sample_s']:.2f}s) scaled x{step} -> {r['frame_est_s']:.2f}s/frame"),
+                detail=r)
+
+
+def load_pmc(kernel: str):
+    """HBM traffic per launch from the committed rocprofv3 PMC summary (FETCH_SIZE doubled per
+    the gfx950 correction + WRITE_SIZE), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--clean", action="store_true", help="GS_FLAG_CLEAN: reference quirks fixed")
+    ap.add_argument("--fast-exp", action="store_true", help="GS_FLAG_FAST_EXP: hardware exp in the blend")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sort-bench", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    world, rank, local, pg = dist_setup()
+    import openglgaussiansplattingrenderer_amd as g
+
+    cfg = CONFIGS[args.config]
+    W, H = cfg["W"], cfg["H"]
+    flags = (g.GS_FLAG_CLEAN if args.clean else 0) | (g.GS_FLAG_FAST_EXP if args.fast_exp else 0)
+    ctx = g.Context(local)
+    sp, data_desc = load_scene(args.config, W, H, ctx, flags)
+    u = camera_for_rank(W, H, rank).uniforms()
+
+    for _ in range(args.warmup):
+        sp.render_uniforms(u)
+    ctx.sync()
+    barrier(pg)
+    ctx.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sp.render_uniforms(u)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier(pg)
+    local_s = t1 - t0
+    elapsed = max_over_ranks(pg, local_s)
+    tm = ctx.timing_read()
+    st = sp.stats
+    N, V, D, E = int(st.num_splats), int(st.visible), int(st.duplicates), int(st.entries)
+    frames_total = world * args.steps
+    value = frames_total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # per-stage average device time over the timed frames (hipEvents on the ctx stream)
+    nf = max(1, tm["frames"])
+    stage_ms = {k[3:]: tm[k] / nf for k in ("ms_preprocess", "ms_emit", "ms_sort", "ms_bins", "ms_draw")}
+    # algorithmic bytes per launch, fp32 SoA, 4-B payload
+    alg = {
+        "preprocess": 40 * N + 24 * V,
+        "emit": 8 * E,
+        "sort": 68 * E,
+        "bins": 4 * E + 1024,
+        "draw": 40 * E + 4 * W * H,
+    }
+    dom = max(stage_ms, key=lambda k: stage_ms[k])
+    kern_name = {"preprocess": "k_preprocess", "emit": "k_emit", "sort": "k_downsweep", "bins": "k_bins_count",
+                 "draw": "k_draw"}[dom]
+    achieved = alg[dom] / (stage_ms[dom] * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "kernel": kern_name, "stage": dom, "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": int(alg[dom]), "avg_launch_ms": round(stage_ms[dom], 4),
+                "traffic": load_pmc(kern_name)}
+    frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
+    frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
+
+    sort = None
+    if not args.no_sort_bench and rank == 0:
+        sort = sort_bench(ctx)
+    cpu = None
+    if not args.no_cpu_baseline and rank == 0 and world == 1:
+        cpu = cpu_baseline(sp, u, flags, budget_s=args.cpu_budget)
+        cpu.pop("detail", None)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": data_desc,
+            "config": {"workload": cfg["desc"] + (" (clean mode)" if args.clean else " (ref mode)") +
+                       (", fast exp" if args.fast_exp else ", defined exp"),
+                       "splats": N, "width": W, "height": H, "views_per_gpu": 1,
+                       "parallelism": f"replicas x{world} (independent views, no collective)"},
+            "frame": {"V": V, "D": D, "E": E, "D_over_N": round(D / max(N, 1), 4),
+                      "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+                      "frame_hbm_frac_algorithmic": round(frame_frac, 4)},
+            "roofline": roofline,
+            "sort": sort,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if pg is not None:
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -166,10 +166,24 @@ int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n
 /* PadBuffer (include/sort.h:23, src/sort.cpp:127-137) */
 int gs_pad_buffer(int size, int unit_width);
 
-/* time the last launch of a kernel class in ms (GS_FLAG_TIMING frames / sorts) */
+/* device time (hipEvents on the ctx stream) of the last draw launch / last standalone sort */
 #define GS_KERNEL_DRAW 1
 #define GS_KERNEL_SORT 2
 int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms);
+
+/* per-stage device time summed over every frame since gs_timing_reset (events recorded on
+ * the ctx stream around each stage; read back without adding syncs to the frame loop) */
+typedef struct gs_timing {
+    int64_t frames;
+    double ms_preprocess;  /* preprocess kernel + block-sum scan */
+    double ms_emit;        /* entry emission */
+    double ms_sort;        /* 4-pass radix sort of the entries */
+    double ms_bins;        /* tile bins */
+    double ms_draw;        /* blend */
+    double ms_frame;       /* first to last event of the frame (includes the E readback gap) */
+} gs_timing;
+int gs_timing_reset(gs_ctx *ctx);
+int gs_timing_read(gs_ctx *ctx, gs_timing *out);
 
 #ifdef __cplusplus
 }

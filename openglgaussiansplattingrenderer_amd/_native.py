@@ -73,6 +73,18 @@ class gs_camera(ctypes.Structure):
     ]
 
 
+class gs_timing(ctypes.Structure):
+    _fields_ = [
+        ("frames", ctypes.c_int64),
+        ("ms_preprocess", ctypes.c_double),
+        ("ms_emit", ctypes.c_double),
+        ("ms_sort", ctypes.c_double),
+        ("ms_bins", ctypes.c_double),
+        ("ms_draw", ctypes.c_double),
+        ("ms_frame", ctypes.c_double),
+    ]
+
+
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -115,6 +127,8 @@ SIGNATURES = {
     "gs_sort_pairs_u32": (_i, [_vp, _vp, _vp, _i64]),
     "gs_pad_buffer": (_i, [_i, _i]),
     "gs_last_kernel_ms": (_i, [_vp, _i, _fp]),
+    "gs_timing_reset": (_i, [_vp]),
+    "gs_timing_read": (_i, [_vp, ctypes.POINTER(gs_timing)]),
 }
 
 _lib = None

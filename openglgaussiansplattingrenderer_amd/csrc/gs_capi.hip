@@ -9,6 +9,10 @@
 #include <string>
 #include <vector>
 
+// frame events: 0 start, 1 preprocess+scan done, 2 emit start, 3 emit done,
+// 4 sort start, 5 sort done, 6 bins done, 7 draw start, 8 draw done
+constexpr int kEv = 9;
+
 struct gs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -41,9 +45,13 @@ struct gs_ctx {
     int n = 0;
     int64_t V = 0, D = 0, E = 0;
     uint32_t flags = 0;
-    // timing
-    hipEvent_t ev[8] = {};
-    float last_draw_ms = 0.f, last_sort_ms = 0.f;
+    // timing: two event sets (frame parity) so frame f-1's events are read after frame f's
+    // mid-frame sync without an extra stall; evs = standalone sort calls
+    hipEvent_t ev[2][kEv] = {};
+    hipEvent_t evs[2] = {};
+    int cur = 0;           // event set of the frame in flight
+    bool pending = false;  // a finished frame's events not yet accumulated
+    gs_timing acc = {};
 };
 
 struct gs_scene {
@@ -134,7 +142,28 @@ gs::SceneDev scene_dev(const gs_scene *s) {
     return d;
 }
 
-bool timing(const gs_ctx *ctx) { return (ctx->flags & GS_FLAG_TIMING) != 0; }
+float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+// fold a completed frame's events into the accumulators
+void accumulate(gs_ctx *ctx, int set) {
+    hipEvent_t *e = ctx->ev[set];
+    ctx->acc.frames += 1;
+    ctx->acc.ms_preprocess += elapsed(e[0], e[1]);
+    ctx->acc.ms_emit += elapsed(e[2], e[3]);
+    ctx->acc.ms_sort += elapsed(e[4], e[5]);
+    ctx->acc.ms_bins += elapsed(e[5], e[6]);
+    ctx->acc.ms_draw += elapsed(e[7], e[8]);
+    ctx->acc.ms_frame += elapsed(e[0], e[8]);
+}
+
+int rec(gs_ctx *ctx, int i) {
+    GS_HIP(ctx, hipEventRecord(ctx->ev[ctx->cur][i], ctx->stream));
+    return GS_OK;
+}
 
 }  // namespace
 
@@ -172,7 +201,10 @@ int gs_ctx_create(int device, gs_ctx **out) {
     if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
-    for (auto &e : ctx->ev)
+    for (auto &set : ctx->ev)
+        for (auto &e : set)
+            if (hipEventCreate(&e) != hipSuccess) return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
+    for (auto &e : ctx->evs)
         if (hipEventCreate(&e) != hipSuccess) return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
     *out = ctx;
     return GS_OK;
@@ -188,7 +220,10 @@ void gs_ctx_destroy(gs_ctx *ctx) {
         if (b) (void)hipFree(b);
     if (ctx->h_totals) (void)hipHostFree(ctx->h_totals);
     gs::sort_free(ctx->sort);
-    for (auto &e : ctx->ev)
+    for (auto &set : ctx->ev)
+        for (auto &e : set)
+            if (e) (void)hipEventDestroy(e);
+    for (auto &e : ctx->evs)
         if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -344,23 +379,30 @@ int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint
     P.n = n;
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = (n + 255) / 256;
-    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[0], ctx->stream));
+    const int prev = ctx->cur;
+    const bool had_pending = ctx->pending;
+    ctx->cur ^= 1;
+    ctx->pending = false;
+    if (int rc = rec(ctx, 0)) return rc;
     GS_HIP(ctx, hipMemsetAsync(ctx->totals, 0, 16, ctx->stream));
     gs::launch_preprocess(ctx->stream, P, scene_dev(scene), fr);
     if (nb > 0) gs::launch_scan_blocksums(ctx->stream, fr, nb);
     GS_HIP(ctx, hipGetLastError());
+    if (int rc = rec(ctx, 1)) return rc;
     // E is needed on the host to size the sort (the reference maps its atomic counter back
     // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
     GS_HIP(ctx, hipMemcpyAsync(ctx->h_totals, ctx->totals, 8, hipMemcpyDeviceToHost, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (had_pending) accumulate(ctx, prev);  // the previous frame has completed
     ctx->V = ctx->h_totals[0];
     ctx->D = ctx->h_totals[1];
     ctx->E = ctx->V + ctx->D;
     if (ctx->E >= ((int64_t)1 << 31)) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: more than 2^31 entries");
     if (int rc = ensure_entries(ctx, ctx->E)) return rc;
+    if (int rc = rec(ctx, 2)) return rc;
     gs::launch_emit(ctx->stream, n, fr, ctx->keys, ctx->vals);
     GS_HIP(ctx, hipGetLastError());
-    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[1], ctx->stream));
+    if (int rc = rec(ctx, 3)) return rc;
     ctx->n = n;
     ctx->stage = 1;
     if (stats) {
@@ -376,9 +418,9 @@ int gs_sort(gs_ctx *ctx) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_sort: call gs_preprocess first");
     if (int rc = use_device(ctx)) return rc;
-    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    if (int rc = rec(ctx, 4)) return rc;
     if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, ctx->E, ctx->err)) return set_error(ctx, rc, ctx->err);
-    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    if (int rc = rec(ctx, 5)) return rc;
     ctx->stage = 2;
     return GS_OK;
 }
@@ -390,7 +432,7 @@ int gs_compute_bins(gs_ctx *ctx) {
     GS_HIP(ctx, hipMemsetAsync(ctx->bin_counts, 0, 256 * 4, ctx->stream));
     gs::launch_bins(ctx->stream, ctx->keys, ctx->E, ctx->bin_counts, ctx->bins);
     GS_HIP(ctx, hipGetLastError());
-    if (timing(ctx)) GS_HIP(ctx, hipEventRecord(ctx->ev[4], ctx->stream));
+    if (int rc = rec(ctx, 6)) return rc;
     ctx->stage = 3;
     return GS_OK;
 }
@@ -443,11 +485,12 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
         dst = ctx->img;
     }
     if (coverW < width || coverH < height) GS_HIP(ctx, hipMemsetAsync(dst, 0, npx * 4, ctx->stream));
-    GS_HIP(ctx, hipEventRecord(ctx->ev[5], ctx->stream));
+    if (int rc = rec(ctx, 7)) return rc;
     gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), scene->colour,
                     dst);
     GS_HIP(ctx, hipGetLastError());
-    GS_HIP(ctx, hipEventRecord(ctx->ev[6], ctx->stream));
+    if (int rc = rec(ctx, 8)) return rc;
+    ctx->pending = true;
     if (!out_on_device) {
         GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
         GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -466,22 +509,15 @@ int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t
     if ((rc = gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
                       out_rgba8, out_on_device)))
         return rc;
-    if (timing(ctx)) {
-        GS_HIP(ctx, hipEventSynchronize(ctx->ev[6]));
-        float a = 0, b = 0, c = 0, d = 0, t = 0;
-        (void)hipEventElapsedTime(&a, ctx->ev[0], ctx->ev[1]);
-        (void)hipEventElapsedTime(&b, ctx->ev[2], ctx->ev[3]);
-        (void)hipEventElapsedTime(&c, ctx->ev[3], ctx->ev[4]);
-        (void)hipEventElapsedTime(&d, ctx->ev[5], ctx->ev[6]);
-        (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[6]);
-        ctx->last_draw_ms = d;
-        ctx->last_sort_ms = b;
+    if (flags & GS_FLAG_TIMING) {
+        hipEvent_t *e = ctx->ev[ctx->cur];
+        GS_HIP(ctx, hipEventSynchronize(e[8]));
         if (stats) {
-            stats->ms_preprocess = a;
-            stats->ms_sort = b;
-            stats->ms_bins = c;
-            stats->ms_draw = d;
-            stats->ms_total = t;
+            stats->ms_preprocess = elapsed(e[0], e[1]) + elapsed(e[2], e[3]);
+            stats->ms_sort = elapsed(e[4], e[5]);
+            stats->ms_bins = elapsed(e[5], e[6]);
+            stats->ms_draw = elapsed(e[7], e[8]);
+            stats->ms_total = elapsed(e[0], e[8]);
         }
     }
     return GS_OK;
@@ -521,29 +557,48 @@ int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n
         if (int rc = grow(ctx, ctx->ask, (size_t)n + (size_t)n / 4)) return rc;
         ctx->ask_cap = (size_t)n + (size_t)n / 4;
     }
-    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    GS_HIP(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
     gs::launch_gather_keys(ctx->stream, d_keys, d_order, ctx->ask, n);
     if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->ask, (uint32_t *)d_order, n, ctx->err))
         return set_error(ctx, rc, ctx->err);
-    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    GS_HIP(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     return GS_OK;
 }
 
 int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n) {
     if (!ctx || (n > 0 && (!d_keys || !d_vals)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_sort_pairs_u32: bad argument");
     if (int rc = use_device(ctx)) return rc;
-    GS_HIP(ctx, hipEventRecord(ctx->ev[2], ctx->stream));
+    GS_HIP(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
     if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, d_keys, d_vals, n, ctx->err)) return set_error(ctx, rc, ctx->err);
-    GS_HIP(ctx, hipEventRecord(ctx->ev[3], ctx->stream));
+    GS_HIP(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     return GS_OK;
 }
 
 int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
     if (!ctx || !ms) return set_error(ctx, GS_ERR_INVALID, "null argument");
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (kernel == GS_KERNEL_DRAW) GS_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[5], ctx->ev[6]));
-    else if (kernel == GS_KERNEL_SORT) GS_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[2], ctx->ev[3]));
+    if (kernel == GS_KERNEL_DRAW) *ms = elapsed(ctx->ev[ctx->cur][7], ctx->ev[ctx->cur][8]);
+    else if (kernel == GS_KERNEL_SORT) *ms = elapsed(ctx->evs[0], ctx->evs[1]);
     else return set_error(ctx, GS_ERR_INVALID, "unknown kernel");
+    return GS_OK;
+}
+
+int gs_timing_reset(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->pending = false;
+    ctx->acc = gs_timing{};
+    return GS_OK;
+}
+
+int gs_timing_read(gs_ctx *ctx, gs_timing *out) {
+    if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pending) {
+        accumulate(ctx, ctx->cur);
+        ctx->pending = false;
+    }
+    *out = ctx->acc;
     return GS_OK;
 }
 

@@ -46,6 +46,14 @@ class Context:
     def sync(self):
         check(lib().gs_sync(self.handle), self.handle)
 
+    def timing_reset(self):
+        check(lib().gs_timing_reset(self.handle), self.handle)
+
+    def timing_read(self) -> dict:
+        t = N.gs_timing()
+        check(lib().gs_timing_read(self.handle, ctypes.byref(t)), self.handle)
+        return {k: getattr(t, k) for k, _ in N.gs_timing._fields_}
+
     def last_kernel_ms(self, kernel: int) -> float:
         ms = ctypes.c_float()
         check(lib().gs_last_kernel_ms(self.handle, kernel, ctypes.byref(ms)), self.handle)

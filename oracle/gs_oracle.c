@@ -429,14 +429,22 @@ void ora_draw(int W, int H, uint32_t flags, const uint32_t *bins256, const uint3
               int64_t E, const float *means2d, const float *conic4, const float *colours4,
               uint8_t *rgba)
 {
+    ora_draw_rows(W, H, flags, bins256, vals, E, means2d, conic4, colours4, rgba, 0, 1);
+}
+
+void ora_draw_rows(int W, int H, uint32_t flags, const uint32_t *bins256, const uint32_t *vals,
+                   int64_t E, const float *means2d, const float *conic4, const float *colours4,
+                   uint8_t *rgba, int row_start, int row_step)
+{
     const int clean = (flags & ORA_FLAG_CLEAN) != 0;
     /* src/Splats.cpp:596 tile size passed as float(W)/16.f, float(H)/16.f */
     const float tileWidth = (float)W / 16.f, tileHeight = (float)H / 16.f;
     /* Q9: the dispatch is (W/32) x (H/32) groups of 32x32 */
     const int coverW = clean ? W : (W / 32) * 32, coverH = clean ? H : (H / 32) * 32;
     memset(rgba, 0, (size_t)W * H * 4);
+    if (row_step < 1) row_step = 1;
 #pragma omp parallel for schedule(dynamic, 1)
-    for (int y = 0; y < coverH; ++y) {
+    for (int y = row_start; y < coverH; y += row_step) {
         for (int x = 0; x < coverW; ++x) {
             float cr = 0.f, cg = 0.f, cbl = 0.f, ca = 0.f;
             /* :78-89 */

@@ -89,6 +89,11 @@ void ora_draw(int W, int H, uint32_t flags, const uint32_t *bins256, const uint3
               int64_t E, const float *means2d, const float *conic4, const float *colours4,
               uint8_t *rgba);
 
+/* same, only rows row_start, row_start + row_step, ... (bounded CPU-baseline samples) */
+void ora_draw_rows(int W, int H, uint32_t flags, const uint32_t *bins256, const uint32_t *vals,
+                   int64_t E, const float *means2d, const float *conic4, const float *colours4,
+                   uint8_t *rgba, int row_start, int row_step);
+
 /* the exp used by the blend (draw.glsl:122); exported for tests */
 float ora_expf(float x);
 

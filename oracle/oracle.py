@@ -44,6 +44,8 @@ def lib():
             "ora_emit": (ctypes.c_int64, [ctypes.c_int, vp, vp, vp, vp, vp, vp, ctypes.c_int64]),
             "ora_bins": (None, [vp, ctypes.c_int64, vp]),
             "ora_draw": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_int64, vp, vp, vp, vp]),
+            "ora_draw_rows": (None, [ctypes.c_int, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_int64, vp, vp, vp,
+                                     vp, ctypes.c_int, ctypes.c_int]),
             "ora_expf": (ctypes.c_float, [ctypes.c_float]),
             "ora_num_threads": (ctypes.c_int, []),
         }
@@ -148,3 +150,44 @@ def render(means4, cov6, opacity, colours4, u, flags: int = 0, stages: bool = Tr
     if stages:
         out["emitted_keys"], out["emitted_vals"] = emitted
     return out
+
+
+def time_frame(means4, cov6, opacity, colours4, u, flags: int = 0, row_step: int = 1) -> dict:
+    """Time the oracle's frame stages (wall clock, host cores).  The blend is run on every
+    ``row_step``-th pixel row only and its time scaled by row_step (a bounded sample)."""
+    import time
+    L = lib()
+    means4 = np.ascontiguousarray(means4, np.float32)
+    cov6 = np.ascontiguousarray(cov6, np.float32)
+    opacity = np.ascontiguousarray(opacity, np.float32)
+    colours4 = np.ascontiguousarray(colours4, np.float32)
+    n = len(opacity)
+    view = np.array(u.view[:], np.float32)
+    vp = np.array(u.vp[:], np.float32)
+    W, H = int(u.width), int(u.height)
+    m2d = np.zeros(2 * n, np.float32)
+    conic = np.zeros(4 * n, np.float32)
+    z01 = np.zeros(n, np.float32)
+    txy = np.zeros(2 * n, np.int32)
+    rect = np.zeros(4 * n, np.int32)
+    cnt = np.zeros(2 * n, np.int32)
+    t0 = time.perf_counter()
+    L.ora_preprocess(n, _p(means4), _p(cov6), _p(opacity), _p(view), _p(vp), W, H, u.focal_x, u.focal_y,
+                     u.tan_fov_x, u.tan_fov_y, flags, _p(m2d), _p(conic), _p(z01), _p(txy), _p(rect), _p(cnt))
+    E = int(L.ora_emit(n, _p(z01), _p(txy), _p(rect), _p(cnt), None, None, 0))
+    keys = np.zeros(max(E, 1), np.uint32)
+    vals = np.zeros(max(E, 1), np.uint32)
+    L.ora_emit(n, _p(z01), _p(txy), _p(rect), _p(cnt), _p(keys), _p(vals), E)
+    t1 = time.perf_counter()
+    L.ora_sort_pairs(_p(keys), _p(vals), E)
+    t2 = time.perf_counter()
+    bins = np.zeros(256, np.uint32)
+    L.ora_bins(_p(keys), E, _p(bins))
+    t3 = time.perf_counter()
+    img = np.zeros((H, W, 4), np.uint8)
+    L.ora_draw_rows(W, H, flags, _p(bins), _p(vals), E, _p(m2d), _p(conic), _p(colours4), _p(img), 0, row_step)
+    t4 = time.perf_counter()
+    draw_full = (t4 - t3) * row_step
+    total = (t1 - t0) + (t2 - t1) + (t3 - t2) + draw_full
+    return dict(preprocess_s=t1 - t0, sort_s=t2 - t1, bins_s=t3 - t2, draw_sample_s=t4 - t3, draw_est_s=draw_full,
+                frame_est_s=total, E=E, row_step=row_step, threads=L.ora_num_threads())
