@@ -34,6 +34,7 @@ struct gs_ctx {
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
     uint32_t *bins = nullptr;        // [256]
+    unsigned long long *draw_stats = nullptr;  // [8] GS_FLAG_DRAW_STATS counters
     // output staging (host-destination renders)
     uint32_t *img = nullptr;
     size_t img_cap = 0;
@@ -45,6 +46,7 @@ struct gs_ctx {
     int n = 0;
     int64_t V = 0, D = 0, E = 0;
     uint32_t flags = 0;
+    int draw_q = 4;  // tuning knob (gs_set_param)
     // timing: two event sets (frame parity) so frame f-1's events are read after frame f's
     // mid-frame sync without an extra stall; evs = standalone sort calls
     hipEvent_t ev[2][kEv] = {};
@@ -199,7 +201,8 @@ int gs_ctx_create(int device, gs_ctx **out) {
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
     if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess)
+        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess ||
+        hipMalloc(&ctx->draw_stats, 128) != hipSuccess || hipMemset(ctx->draw_stats, 0, 128) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
     for (auto &set : ctx->ev)
         for (auto &e : set)
@@ -215,7 +218,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     void *bufs[] = {ctx->m2d, ctx->conic, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
-                    ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask};
+                    ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->h_totals) (void)hipHostFree(ctx->h_totals);
@@ -451,6 +454,7 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     P.E = (int32_t)ctx->E;
     P.clean = clean ? 1 : 0;
     P.no_cull = (flags & GS_FLAG_NO_CULL) ? 1 : 0;
+    P.q = ctx->draw_q;
     // Q9: the reference dispatches (W/32) x (H/32) workgroups of 32x32 pixels
     const int coverW = clean ? width : (width / 32) * 32;
     const int coverH = clean ? height : (height / 32) * 32;
@@ -487,7 +491,7 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     if (coverW < width || coverH < height) GS_HIP(ctx, hipMemsetAsync(dst, 0, npx * 4, ctx->stream));
     if (int rc = rec(ctx, 7)) return rc;
     gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), scene->colour,
-                    dst);
+                    dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr);
     GS_HIP(ctx, hipGetLastError());
     if (int rc = rec(ctx, 8)) return rc;
     ctx->pending = true;
@@ -580,6 +584,24 @@ int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
     if (kernel == GS_KERNEL_DRAW) *ms = elapsed(ctx->ev[ctx->cur][7], ctx->ev[ctx->cur][8]);
     else if (kernel == GS_KERNEL_SORT) *ms = elapsed(ctx->evs[0], ctx->evs[1]);
     else return set_error(ctx, GS_ERR_INVALID, "unknown kernel");
+    return GS_OK;
+}
+
+int gs_set_param(gs_ctx *ctx, int param, int value) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (param == GS_PARAM_DRAW_Q) {
+        if (value != 2 && value != 4 && value != 8) return set_error(ctx, GS_ERR_INVALID, "draw_q must be 2, 4 or 8");
+        ctx->draw_q = value;
+        return GS_OK;
+    }
+    return set_error(ctx, GS_ERR_INVALID, "unknown parameter");
+}
+
+int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset) {
+    if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
+    GS_HIP(ctx, hipMemcpyAsync(out, ctx->draw_stats, 128, hipMemcpyDeviceToHost, ctx->stream));
+    if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, 128, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return GS_OK;
 }
 

@@ -47,6 +47,7 @@ struct DrawParams {
     int32_t clean;
     int32_t no_cull;
     int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
+    int32_t q;                  // list entries per lane per iteration (2, 4, 8)
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };
@@ -88,6 +89,6 @@ void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks);
 void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals);
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins);
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out);
+                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats);
 
 }  // namespace gs

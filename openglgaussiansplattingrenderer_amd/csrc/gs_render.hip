@@ -356,115 +356,202 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict
 }
 
 // ---------------------------------------------------------------------- draw
-// One 256-thread workgroup per 16x16 pixel sub-block of a coarse tile (blocks never
-// straddle coarse tiles, so each pixel blends exactly its own tile's list -- Q18 resolved).
-// The tile's sorted list is streamed in chunks of 256 entries: each lane tests one entry's
-// conservative box against the sub-block, survivors are compacted in order into LDS, then
-// every pixel blends the compacted chunk front to back.  Entries the cull drops would be
-// skipped by draw.glsl:118-126 at every pixel of the sub-block, so results are unchanged.
-template <bool FAST_EXP>
-__global__ __launch_bounds__(kBlock) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
-                                                 const uint32_t *__restrict__ vals, const float2 *__restrict__ m2d,
-                                                 const float4 *__restrict__ conic, const float4 *__restrict__ cullbox,
-                                                 const float4 *__restrict__ colour, uint32_t *__restrict__ out) {
-    __shared__ float4 s_p0[kBlock];  // mx, my, conic.x, conic.y
-    __shared__ float4 s_p1[kBlock];  // conic.z, opacity, r, g
-    __shared__ float s_p2[kBlock];   // b
-    __shared__ uint32_t s_wcnt[kBlock / 64];
+// One wave (64-thread workgroup) per 16x16 pixel sub-block of a coarse tile; lane l owns
+// the 2x2 pixel quad at (2*(l%8), 2*(l/8)), so one survivor's LDS reads and the per-column
+// (a*dx)*dx / per-row (c*dy)*dy products serve four pixels (each pixel's arithmetic is the
+// same sequence of IEEE ops as draw.glsl / the oracle).  Sub-blocks never straddle coarse
+// tiles, so each pixel blends exactly its own tile's list (Q18 resolved).
+// Per iteration the wave takes Q*64 entries of the tile's sorted list (next iteration's
+// indices prefetched), gathers each entry's conservative box and keeps those touching the
+// sub-block; survivors are compacted IN ORDER into wave-private LDS and blended front to
+// back.  Both filters only drop work draw.glsl would `continue` past (draw.glsl:118-126):
+//   * box cull: the entry's alpha >= 1/255 region misses the sub-block;
+//   * pre-exp skip: power < ln(1/(255*o)) - 1e-3 implies alpha < 1/255 for any exp
+//     within a few ulp.
+// Block placement is XCD-aware: workgroups are dealt round-robin over the 8 XCDs (block b
+// and b+8 share one), so linear block id L maps to XCD L % 8 and all sub-blocks of coarse
+// tile t go to XCD t % 8, consecutively, gathering the tile's list through one L2 (speed
+// only; any placement gives the same pixels).
+constexpr int kCap = 128;  // survivors staged in LDS per round
 
-    const int tx = blockIdx.x / P.nbx, sbx = blockIdx.x - tx * P.nbx;
-    const int ty = blockIdx.y / P.nby, sby = blockIdx.y - ty * P.nby;
+template <bool FAST_EXP>
+__device__ __forceinline__ void blend_px(float power, float o, float r, float g, float b, float4 &col, bool &done) {
+    const float e = FAST_EXP ? __expf(power) : exp_defined(power);
+    const float alpha = fminf(0.99f, e * o);
+    if (alpha < 1.0f / 255.0f) return;
+    // alphaBlend :59-67
+    const float remaining = 1.0f - col.w;
+    const float aT = alpha * remaining;
+    col.x = col.x + r * aT;
+    col.y = col.y + g * aT;
+    col.z = col.z + b * aT;
+    col.w = col.w + aT;
+    if (col.w >= 0.99f) done = true;  // :129-133
+}
+
+__device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
+    // :141-142 imageStore(rgba8, col / 255): unorm, round to nearest
+    const float vv[4] = {c.x / 255.0f, c.y / 255.0f, c.z / 255.0f, c.w / 255.0f};
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float q = vv[k];
+        q = (q != q) ? 0.0f : q;
+        q = q < 0.0f ? 0.0f : (q > 1.0f ? 1.0f : q);
+        packed |= ((uint32_t)floorf(q * 255.0f + 0.5f)) << (8 * k);
+    }
+    return packed;
+}
+
+template <bool FAST_EXP, bool STATS, int Q>
+__global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
+                                             const uint32_t *__restrict__ vals, const float2 *__restrict__ m2d,
+                                             const float4 *__restrict__ conic, const float4 *__restrict__ cullbox,
+                                             const float4 *__restrict__ colour, uint32_t *__restrict__ out,
+                                             unsigned long long *__restrict__ stats) {
+    constexpr int kChunk = Q * 64;
+    __shared__ float4 s_p0[kCap];  // mx, my, conic.x, conic.y
+    __shared__ float4 s_p1[kCap];  // conic.z, opacity, r, g
+    __shared__ float2 s_p2[kCap];  // b, pre-exp skip threshold
+
+    const int nsub = P.nbx * P.nby;
+    const int L = blockIdx.x;
+    const int xcd = L & 7, kk = L >> 3;
+    const int t = xcd + 8 * (kk / nsub);  // coarse tile (t % 8 == xcd)
+    const int sub = kk - (kk / nsub) * nsub;
+    const int tx = t & 15, ty = t >> 4;
+    const int sby = sub / P.nbx, sbx = sub - sby * P.nbx;
     const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
     const int x0 = P.xb[tx] + sbx * 16, y0 = P.yb[ty] + sby * 16;
     if (x0 >= xe || y0 >= ye) return;  // uniform: sub-block beyond this tile
     const int x1 = min(x0 + 16, xe), y1 = min(y0 + 16, ye);
-    const int px = x0 + (threadIdx.x & 15), py = y0 + (threadIdx.x >> 4);
-    const bool inside = px < x1 && py < y1;
-    const float fpx = (float)px, fpy = (float)py;
+    const int lane = threadIdx.x;
+    const int pxa = x0 + 2 * (lane & 7), pya = y0 + 2 * (lane >> 3);
+    const bool in00 = pxa < x1 && pya < y1, in10 = pxa + 1 < x1 && pya < y1;
+    const bool in01 = pxa < x1 && pya + 1 < y1, in11 = pxa + 1 < x1 && pya + 1 < y1;
+    const float fx0 = (float)pxa, fx1 = (float)(pxa + 1), fy0 = (float)pya, fy1 = (float)(pya + 1);
     const float bx0 = (float)x0, bx1 = (float)(x1 - 1), by0 = (float)y0, by1 = (float)(y1 - 1);
 
-    const int t = ty * 16 + tx;
     const int start = (t == 0) ? 0 : (int)bins[t - 1];
     int end = (int)bins[t];
     if (!P.clean && end > start) {  // Q10: the last 1024-entry chunk is blended whole
         const int chunks = (end - start + 1023) / 1024;
         end = min(P.E, start + chunks * 1024);
     }
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    float cr = 0.f, cg = 0.f, cb = 0.f, ca = 0.f;
-    bool done = !inside;
+    float4 c00 = make_float4(0.f, 0.f, 0.f, 0.f), c10 = c00, c01 = c00, c11 = c00;
+    bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
+    unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
+    const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
 
-    for (int base = start; base < end; base += kBlock) {
-        const int j = base + threadIdx.x;
-        bool keep = false;
-        uint32_t v = 0;
-        if (j < end) {
-            v = vals[j];
-            if (P.no_cull) {
-                keep = true;
-            } else {
-                const float4 b = cullbox[v];
-                keep = (b.x <= bx1) && (b.y >= bx0) && (b.z <= by1) && (b.w >= by0);
-            }
-        }
-        const uint64_t bal = __ballot(keep);
-        if (lane == 0) s_wcnt[wid] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t woff = 0, total = 0;
+    uint32_t v[Q];
 #pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) {
-            const uint32_t c = s_wcnt[w];
-            woff += (w < wid) ? c : 0u;
-            total += c;
-        }
-        if (keep) {
-            const uint32_t pos = woff + (uint32_t)__popcll(bal & lanemask_lt());
-            const float2 m = m2d[v];
-            const float4 co = conic[v];
-            const float4 col = colour[v];
-            s_p0[pos] = make_float4(m.x, m.y, co.x, co.y);
-            s_p1[pos] = make_float4(co.z, co.w, col.x, col.y);
-            s_p2[pos] = col.z;
-        }
-        __syncthreads();
-        if (!done) {
-            for (uint32_t k = 0; k < total; ++k) {
-                const float4 a = s_p0[k];
-                const float4 b = s_p1[k];
-                // :111-126
-                const float dx = fpx - a.x, dy = fpy - a.y;
-                const float power = -0.5f * (a.z * dx * dx + b.x * dy * dy) - a.w * dx * dy;
-                if (power > 0.0f) continue;
-                const float e = FAST_EXP ? __expf(power) : exp_defined(power);
-                const float alpha = fminf(0.99f, e * b.y);
-                if (alpha < 1.0f / 255.0f) continue;
-                // alphaBlend :59-67
-                const float remaining = 1.0f - ca;
-                const float aT = alpha * remaining;
-                cr = cr + b.z * aT;
-                cg = cg + b.w * aT;
-                cb = cb + s_p2[k] * aT;
-                ca = ca + aT;
-                if (ca >= 0.99f) {  // :129-133
-                    done = true;
-                    break;
+    for (int q = 0; q < Q; ++q) {
+        const int j = start + q * 64 + lane;
+        v[q] = (j < end) ? vals[j] : 0xffffffffu;
+    }
+    for (int base = start; base < end; base += kChunk) {
+        bool keep[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            keep[q] = false;
+            if (v[q] != 0xffffffffu) {
+                if (P.no_cull) {
+                    keep[q] = true;
+                } else {
+                    const float4 b = cullbox[v[q]];
+                    keep[q] = (b.x <= bx1) && (b.y >= bx0) && (b.z <= by1) && (b.w >= by0);
                 }
             }
         }
-        if (__syncthreads_and(done ? 1 : 0)) break;  // every pixel saturated: nothing can change
-    }
-    if (inside) {
-        // :141-142 imageStore(rgba8, col / 255): unorm, round to nearest
-        const float vv[4] = {cr / 255.0f, cg / 255.0f, cb / 255.0f, ca / 255.0f};
-        uint32_t packed = 0;
+        uint32_t vn[Q];  // prefetch the next iteration's entry indices
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            float q = vv[c];
-            q = (q != q) ? 0.0f : q;
-            q = q < 0.0f ? 0.0f : (q > 1.0f ? 1.0f : q);
-            packed |= ((uint32_t)floorf(q * 255.0f + 0.5f)) << (8 * c);
+        for (int q = 0; q < Q; ++q) {
+            const int j = base + kChunk + q * 64 + lane;
+            vn[q] = (j < end) ? vals[j] : 0xffffffffu;
         }
-        out[(size_t)py * P.W + px] = packed;
+        // survivors in list order: (q, lane)
+        uint32_t total = 0, myoff[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint64_t bal = __ballot(keep[q]);
+            myoff[q] = total + (uint32_t)__popcll(bal & lanemask_lt());
+            total += (uint32_t)__popcll(bal);
+        }
+        if (STATS) {
+            ++st_iter;
+            st_surv += total;
+        }
+        for (uint32_t r0 = 0; r0 < total; r0 += kCap) {
+            __syncthreads();  // one-wave workgroup: orders LDS reuse (cheap)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                if (keep[q] && myoff[q] >= r0 && myoff[q] < r0 + kCap) {
+                    const uint32_t pos = myoff[q] - r0;
+                    const float2 m = m2d[v[q]];
+                    const float4 co = conic[v[q]];
+                    const float4 col = colour[v[q]];
+                    s_p0[pos] = make_float4(m.x, m.y, co.x, co.y);
+                    s_p1[pos] = make_float4(co.z, co.w, col.x, col.y);
+                    s_p2[pos] = make_float2(col.z, -logf(255.0f * co.w) - 1.0e-3f);
+                }
+            }
+            __syncthreads();
+            const uint32_t cnt = min((uint32_t)kCap, total - r0);
+            for (uint32_t k = 0; k < cnt; ++k) {
+                if (d00 && d10 && d01 && d11) break;
+                const float4 a = s_p0[k];
+                const float4 b = s_p1[k];
+                const float2 c = s_p2[k];
+                // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
+                const float dx0 = fx0 - a.x, dx1 = fx1 - a.x, dy0 = fy0 - a.y, dy1 = fy1 - a.y;
+                const float ax0 = a.z * dx0 * dx0, ax1 = a.z * dx1 * dx1;
+                const float cy0 = b.x * dy0 * dy0, cy1 = b.x * dy1 * dy1;
+                const float bx0d = a.w * dx0, bx1d = a.w * dx1;
+                const float p00 = -0.5f * (ax0 + cy0) - bx0d * dy0;
+                const float p10 = -0.5f * (ax1 + cy0) - bx1d * dy0;
+                const float p01 = -0.5f * (ax0 + cy1) - bx0d * dy1;
+                const float p11 = -0.5f * (ax1 + cy1) - bx1d * dy1;
+                // :118-126 (power > 0 -> continue), plus the exact pre-exp skip
+                const bool n00 = !d00 && !(p00 > 0.0f) && !(p00 < c.y);
+                const bool n10 = !d10 && !(p10 > 0.0f) && !(p10 < c.y);
+                const bool n01 = !d01 && !(p01 > 0.0f) && !(p01 < c.y);
+                const bool n11 = !d11 && !(p11 > 0.0f) && !(p11 < c.y);
+                if (STATS) {
+                    const uint64_t bn = __ballot(n00 || n10 || n01 || n11);
+                    ++st_kit;
+                    st_anyneed += bn ? 1 : 0;
+                    st_pxneed += __popcll(__ballot(n00)) + __popcll(__ballot(n10)) + __popcll(__ballot(n01)) +
+                                 __popcll(__ballot(n11));
+                }
+                if (n00 || n10 || n01 || n11) {
+                    if (n00) blend_px<FAST_EXP>(p00, b.y, b.z, b.w, c.x, c00, d00);
+                    if (n10) blend_px<FAST_EXP>(p10, b.y, b.z, b.w, c.x, c10, d10);
+                    if (n01) blend_px<FAST_EXP>(p01, b.y, b.z, b.w, c.x, c01, d01);
+                    if (n11) blend_px<FAST_EXP>(p11, b.y, b.z, b.w, c.x, c11, d11);
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; ++q) v[q] = vn[q];
+        if (__all(d00 && d10 && d01 && d11)) break;  // every pixel saturated: nothing can change
+    }
+    if (in00) out[(size_t)pya * P.W + pxa] = pack_rgba8(c00);
+    if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(c10);
+    if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(c01);
+    if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(c11);
+    if (STATS && lane == 0) {
+        const unsigned long long cyc = __builtin_amdgcn_s_memtime() - st_t0;
+        atomicAdd(&stats[0], 1ull);
+        atomicAdd(&stats[1], st_iter);
+        atomicAdd(&stats[2], st_surv);
+        atomicAdd(&stats[3], (unsigned long long)max(0, end - start));
+        atomicMax(&stats[4], st_iter);
+        atomicMax(&stats[5], st_surv);
+        atomicMax(&stats[6], cyc);
+        atomicAdd(&stats[7], cyc);
+        atomicAdd(&stats[8], st_kit);
+        atomicAdd(&stats[9], st_anyneed);
+        atomicAdd(&stats[10], st_pxneed);
     }
 }
 
@@ -492,15 +579,28 @@ void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *count
 }
 
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out) {
-    const dim3 grid(kTiles * P.nbx, kTiles * P.nby);
+                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats) {
+    // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks, XCD-major (see k_draw)
+    const dim3 grid(kTiles * kTiles * P.nbx * P.nby);
     if (P.nbx <= 0 || P.nby <= 0) return;
-    if (fast_exp)
-        hipLaunchKernelGGL(k_draw<true>, grid, dim3(kBlock), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox,
-                           colour, out);
-    else
-        hipLaunchKernelGGL(k_draw<false>, grid, dim3(kBlock), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox,
-                           colour, out);
+#define GS_DRAW(F, S, Q)                                                                                       \
+    hipLaunchKernelGGL((k_draw<F, S, Q>), grid, dim3(64), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox, \
+                       colour, out, stats)
+#define GS_DRAW_Q(F, S)                  \
+    do {                                 \
+        if (P.q == 2) GS_DRAW(F, S, 2);  \
+        else if (P.q == 8) GS_DRAW(F, S, 8); \
+        else GS_DRAW(F, S, 4);           \
+    } while (0)
+    if (stats) {
+        if (fast_exp) GS_DRAW_Q(true, true);
+        else GS_DRAW_Q(false, true);
+    } else {
+        if (fast_exp) GS_DRAW_Q(true, false);
+        else GS_DRAW_Q(false, false);
+    }
+#undef GS_DRAW_Q
+#undef GS_DRAW
 }
 
 }  // namespace gs

@@ -54,6 +54,16 @@ class Context:
         check(lib().gs_timing_read(self.handle, ctypes.byref(t)), self.handle)
         return {k: getattr(t, k) for k, _ in N.gs_timing._fields_}
 
+    def set_param(self, param: int, value: int):
+        check(lib().gs_set_param(self.handle, int(param), int(value)), self.handle)
+
+    def draw_stats(self, reset: bool = True) -> dict:
+        a = np.zeros(16, np.uint64)
+        check(lib().gs_draw_stats(self.handle, ptr(a), int(reset)), self.handle)
+        return dict(blocks=int(a[0]), iterations=int(a[1]), survivors=int(a[2]), list_entries=int(a[3]),
+                    max_iterations=int(a[4]), max_survivors=int(a[5]), max_cycles=int(a[6]), sum_cycles=int(a[7]),
+                    wave_steps=int(a[8]), steps_any_need=int(a[9]), pixel_needs=int(a[10]))
+
     def last_kernel_ms(self, kernel: int) -> float:
         ms = ctypes.c_float()
         check(lib().gs_last_kernel_ms(self.handle, kernel, ctypes.byref(ms)), self.handle)
@@ -106,8 +116,8 @@ class DeviceBuffer:
 def createAndLinkSortAndHistogramShaders():
     """src/sort.cpp:15-124.  Nothing to compile at run time (kernels are built ahead of
     time for gfx950); returns placeholder program handles (histogram, sort, sum)."""
-    print("compiling sorting shaders")
-    print("compiled and linked sorting shaders")
+    print("compiling sorting shaders", file=sys.stderr)
+    print("compiled and linked sorting shaders", file=sys.stderr)
     return 1, 2, 3
 
 
@@ -339,7 +349,7 @@ class Splats:
                  device: int = 0, flags: int = 0, arrays=None):
         self.ctx = ctx if ctx is not None else Context(device)
         self.flags = int(flags)
-        print("setting up splats")
+        print("setting up splats", file=sys.stderr)
         if arrays is None:
             self.loadSplats(filePath)
         else:
@@ -350,7 +360,7 @@ class Splats:
         self.computeCovarianceMatrices()
         self._scene = None
         self.loadToGPU(width, height)
-        print("finished setting up splats")
+        print("finished setting up splats", file=sys.stderr)
 
     @classmethod
     def from_raw(cls, means3, f_dc, opacity_logit, log_scale, rot_raw, width, height, **kw) -> "Splats":
@@ -362,11 +372,11 @@ class Splats:
 
     # src/Splats.cpp:174-344
     def loadSplats(self, filePath: str):
-        print("Loading splats from file")
+        print("Loading splats from file", file=sys.stderr)
         self.means3D, self.colours, self.opacities, self.scales, self.rotations = load_ply(filePath)
         self.numSplats = len(self.means3D)
-        print(f"num splats: {self.numSplats}")
-        print("Finished loading splats from file")
+        print(f"num splats: {self.numSplats}", file=sys.stderr)
+        print("Finished loading splats from file", file=sys.stderr)
 
     # src/Splats.cpp:414-438
     def computeCovarianceMatrices(self):
