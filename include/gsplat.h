@@ -185,7 +185,7 @@ typedef struct gs_timing {
 } gs_timing;
 int gs_timing_reset(gs_ctx *ctx);
 /* tuning knobs (results never depend on them) */
-#define GS_PARAM_DRAW_Q 1  /* blend: list entries per lane per iteration, 2 / 4 / 8 */
+#define GS_PARAM_DRAW_Q 1     /* blend: list entries per lane per pipeline step, 1 / 2 / 4 */
 int gs_set_param(gs_ctx *ctx, int param, int value);
 
 /* blend work counters accumulated by GS_FLAG_DRAW_STATS frames: [0] sub-blocks drawn,

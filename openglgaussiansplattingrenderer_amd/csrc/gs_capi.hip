@@ -46,7 +46,7 @@ struct gs_ctx {
     int n = 0;
     int64_t V = 0, D = 0, E = 0;
     uint32_t flags = 0;
-    int draw_q = 4;  // tuning knob (gs_set_param)
+    int draw_q = 1;  // tuning knob (gs_set_param)
     // timing: two event sets (frame parity) so frame f-1's events are read after frame f's
     // mid-frame sync without an extra stall; evs = standalone sort calls
     hipEvent_t ev[2][kEv] = {};
@@ -102,7 +102,7 @@ int grow(gs_ctx *ctx, T *&p, size_t count) {
 int ensure_splats(gs_ctx *ctx, int n) {
     if (n <= ctx->n_cap) return GS_OK;
     const int cap = n;
-    const int nb = (cap + 255) / 256;
+    const int nb = gs::preprocess_blocks(cap);
     int rc;
     if ((rc = grow(ctx, ctx->m2d, cap)) || (rc = grow(ctx, ctx->conic, cap)) || (rc = grow(ctx, ctx->cullbox, cap)) ||
         (rc = grow(ctx, ctx->rec, cap)) || (rc = grow(ctx, ctx->blocksum, nb)))
@@ -381,7 +381,7 @@ int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint
     }
     P.n = n;
     const gs::FrameDev fr = frame_dev(ctx);
-    const int nb = (n + 255) / 256;
+    const int nb = gs::preprocess_blocks(n);
     const int prev = ctx->cur;
     const bool had_pending = ctx->pending;
     ctx->cur ^= 1;
@@ -590,7 +590,7 @@ int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
 int gs_set_param(gs_ctx *ctx, int param, int value) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (param == GS_PARAM_DRAW_Q) {
-        if (value != 2 && value != 4 && value != 8) return set_error(ctx, GS_ERR_INVALID, "draw_q must be 2, 4 or 8");
+        if (value != 1 && value != 2 && value != 4) return set_error(ctx, GS_ERR_INVALID, "draw_q must be 1, 2 or 4");
         ctx->draw_q = value;
         return GS_OK;
     }

@@ -81,9 +81,10 @@ struct FrameDev {
     float4 *conic;     // conic.xyz, opacity
     float4 *cullbox;   // conservative pixel box of the alpha >= 1/255 region
     int4 *rec;         // z01 bits, tileX, tileY (-1: no entries), packed rect
-    uint2 *blocksum;   // per-256-splat block (main, dup) sums -> exclusive offsets
+    uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
     uint32_t *totals;  // [0]=V [1]=D
 };
+int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks);
 void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals);

@@ -74,7 +74,6 @@ __device__ __forceinline__ float exp_defined(float x) {
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // inclusive wave scan (wave64)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -106,10 +105,17 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w
 }
 
 // ------------------------------------------------------------------ preprocess
+// kPer splats per lane, striped (splat = block*kSplatsPerBlock + k*256 + lane) so every load
+// stays coalesced; one (main, dup) sum per workgroup feeds the emission scan.
+constexpr int kPer = 4;
+constexpr int kSplatsPerBlock = kPer * kBlock;  // 1024
+
 __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_wave[kBlock / 64];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
     uint32_t n_main = 0, n_dup = 0;
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+    const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
     if (i < P.n) {
         const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
         float2 m2 = make_float2(0.f, 0.f);
@@ -183,8 +189,8 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             }
             const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
             const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
-            n_main = 1;
-            n_dup = (uint32_t)(rectCount - mainInRect);
+            n_main += 1;
+            n_dup += (uint32_t)(rectCount - mainInRect);
             const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
                                 ((uint32_t)maxY << 24);
             rc = make_int4((int)f2u(sz), tileX, tileY, (int)rp);
@@ -214,6 +220,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         fr.cullbox[i] = box;
         fr.rec[i] = rc;
     }
+    }
     // block sums of (main, dup) for the emission offsets
     uint32_t tot_main, tot_dup;
     block_excl_scan256(n_main, s_wave, &tot_main);
@@ -221,20 +228,31 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
     if (threadIdx.x == 0) fr.blocksum[blockIdx.x] = make_uint2(tot_main, tot_dup);
 }
 
-// exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1]
+// exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1].
+// One workgroup; each thread owns 16 consecutive sums per round (independent loads issued
+// together), so a round costs one memory round trip instead of one per 1024 sums.
+constexpr int kScanPer = 16;
 __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblocks) {
     __shared__ uint32_t s_w0[16], s_w1[16];
     __shared__ uint32_t s_carry[2];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry[0] = s_carry[1] = 0;
     __syncthreads();
-    for (int base = 0; base < nblocks; base += 1024) {
-        const int i = base + threadIdx.x;
-        const uint2 v = (i < nblocks) ? fr.blocksum[i] : make_uint2(0, 0);
-        const uint32_t i0 = wave_incl_scan(v.x), i1 = wave_incl_scan(v.y);
+    for (int base = 0; base < nblocks; base += 1024 * kScanPer) {
+        const int i0 = base + threadIdx.x * kScanPer;
+        uint2 v[kScanPer];
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) v[k] = (i0 + k < nblocks) ? fr.blocksum[i0 + k] : make_uint2(0, 0);
+        uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            a0 += v[k].x;
+            a1 += v[k].y;
+        }
+        const uint32_t c0 = wave_incl_scan(a0), c1 = wave_incl_scan(a1);
         if (lane == 63) {
-            s_w0[wid] = i0;
-            s_w1[wid] = i1;
+            s_w0[wid] = c0;
+            s_w1[wid] = c1;
         }
         __syncthreads();
         uint32_t o0 = s_carry[0], o1 = s_carry[1], t0 = 0, t1 = 0;
@@ -244,7 +262,14 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblock
             t0 += s_w0[w];
             t1 += s_w1[w];
         }
-        if (i < nblocks) fr.blocksum[i] = make_uint2(o0 + i0 - v.x, o1 + i1 - v.y);
+        o0 += c0 - a0;
+        o1 += c1 - a1;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {
+            if (i0 + k < nblocks) fr.blocksum[i0 + k] = make_uint2(o0, o1);
+            o0 += v[k].x;
+            o1 += v[k].y;
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             s_carry[0] += t0;
@@ -260,43 +285,51 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblock
 
 // ---------------------------------------------------------------------- emit
 // positions: mains [0,V) in splat order, duplicates [V, V+D) splat-major with the rect
-// walked y-major / x-minor and the main tile skipped (preprocess.glsl:171-188)
+// walked y-major / x-minor and the main tile skipped (preprocess.glsl:171-188).  Same
+// striped kPer-per-lane layout as k_preprocess; item order (it, lane) == splat order.
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
                                                  uint32_t *__restrict__ vals) {
     __shared__ uint32_t s_wave[kBlock / 64];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    int4 rc = make_int4(0, -1, -1, 0);
-    if (i < n) rc = fr.rec[i];
-    const bool has = rc.y >= 0;
-    const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
-    const int tileX = rc.y, tileY = rc.z;
-    uint32_t n_main = 0, n_dup = 0;
-    if (has) {
-        const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
-        const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
-        n_main = 1;
-        n_dup = (uint32_t)(rectCount - mainInRect);
-    }
-    uint32_t t0, t1;
-    const uint32_t pm = block_excl_scan256(n_main, s_wave, &t0);
-    const uint32_t pd = block_excl_scan256(n_dup, s_wave, &t1);
-    if (!has) return;
     const uint2 off = fr.blocksum[blockIdx.x];
     const uint32_t V = fr.totals[0];
-    const float z = u2f((uint32_t)rc.x);
-    // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
-    const uint32_t mpos = off.x + pm;
-    const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
-    keys[mpos] = f2u((float)tileIndex + z);
-    vals[mpos] = (uint32_t)i;
-    uint32_t d = V + off.y + pd;
-    for (int y = minY; y <= maxY; ++y)
-        for (int x = minX; x <= maxX; ++x) {
-            if (x == tileX && y == tileY) continue;
-            keys[d] = f2u((float)(uint32_t)(y * 16 + x) + z);
-            vals[d] = (uint32_t)i;
-            ++d;
+    uint32_t carry_m = off.x, carry_d = off.y;
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+        const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
+        int4 rc = make_int4(0, -1, -1, 0);
+        if (i < n) rc = fr.rec[i];
+        const bool has = rc.y >= 0;
+        const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
+        const int tileX = rc.y, tileY = rc.z;
+        uint32_t n_main = 0, n_dup = 0;
+        if (has) {
+            const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+            const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
+            n_main = 1;
+            n_dup = (uint32_t)(rectCount - mainInRect);
         }
+        uint32_t t0, t1;
+        const uint32_t pm = block_excl_scan256(n_main, s_wave, &t0);
+        const uint32_t pd = block_excl_scan256(n_dup, s_wave, &t1);
+        if (has) {
+            const float z = u2f((uint32_t)rc.x);
+            // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
+            const uint32_t mpos = carry_m + pm;
+            const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
+            keys[mpos] = f2u((float)tileIndex + z);
+            vals[mpos] = (uint32_t)i;
+            uint32_t d = V + carry_d + pd;
+            for (int y = minY; y <= maxY; ++y)
+                for (int x = minX; x <= maxX; ++x) {
+                    if (x == tileX && y == tileY) continue;
+                    keys[d] = f2u((float)(uint32_t)(y * 16 + x) + z);
+                    vals[d] = (uint32_t)i;
+                    ++d;
+                }
+        }
+        carry_m += t0;
+        carry_d += t1;
+    }
 }
 
 // ---------------------------------------------------------------------- bins
@@ -357,14 +390,22 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict
 
 // ---------------------------------------------------------------------- draw
 // One wave (64-thread workgroup) per 16x16 pixel sub-block of a coarse tile; lane l owns
-// the 2x2 pixel quad at (2*(l%8), 2*(l/8)), so one survivor's LDS reads and the per-column
-// (a*dx)*dx / per-row (c*dy)*dy products serve four pixels (each pixel's arithmetic is the
-// same sequence of IEEE ops as draw.glsl / the oracle).  Sub-blocks never straddle coarse
-// tiles, so each pixel blends exactly its own tile's list (Q18 resolved).
-// Per iteration the wave takes Q*64 entries of the tile's sorted list (next iteration's
-// indices prefetched), gathers each entry's conservative box and keeps those touching the
-// sub-block; survivors are compacted IN ORDER into wave-private LDS and blended front to
-// back.  Both filters only drop work draw.glsl would `continue` past (draw.glsl:118-126):
+// the 2x2 pixel quad at (2*(l%8), 2*(l/8)).  Sub-blocks never straddle coarse tiles, so
+// each pixel blends exactly its own tile's list (Q18 resolved).
+//
+// The tile's sorted list is consumed Q*64 entries per step through a register pipeline, so
+// the gathers of later steps are in flight while the current step blends:
+//   step i:   keep(i+1) = box(i+1) touches the sub-block;  issue splat-data gathers for the
+//             survivors of i+1, box gathers for i+2, index loads for i+3;  then blend the
+//             survivors of step i (their data arrived during step i-1).
+// Survivors are never staged in LDS: each stays in the registers of the lane that gathered
+// it and is broadcast with v_readlane while the wave walks the ballot mask in ascending
+// lane order -- exactly list order.  Per survivor, every lane evaluates power for its four
+// pixels; the pixels that can blend become (pixel, power) events, compacted and processed
+// one per lane on the pixel state kept in LDS (a pixel occurs at most once per survivor,
+// so events never conflict, and each pixel still sees its survivors in list order).  Each pixel's arithmetic is the same sequence of IEEE
+// ops as draw.glsl / the oracle, and both filters only drop work draw.glsl would `continue`
+// past (draw.glsl:118-126):
 //   * box cull: the entry's alpha >= 1/255 region misses the sub-block;
 //   * pre-exp skip: power < ln(1/(255*o)) - 1e-3 implies alpha < 1/255 for any exp
 //     within a few ulp.
@@ -372,22 +413,6 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict
 // and b+8 share one), so linear block id L maps to XCD L % 8 and all sub-blocks of coarse
 // tile t go to XCD t % 8, consecutively, gathering the tile's list through one L2 (speed
 // only; any placement gives the same pixels).
-constexpr int kCap = 128;  // survivors staged in LDS per round
-
-template <bool FAST_EXP>
-__device__ __forceinline__ void blend_px(float power, float o, float r, float g, float b, float4 &col, bool &done) {
-    const float e = FAST_EXP ? __expf(power) : exp_defined(power);
-    const float alpha = fminf(0.99f, e * o);
-    if (alpha < 1.0f / 255.0f) return;
-    // alphaBlend :59-67
-    const float remaining = 1.0f - col.w;
-    const float aT = alpha * remaining;
-    col.x = col.x + r * aT;
-    col.y = col.y + g * aT;
-    col.z = col.z + b * aT;
-    col.w = col.w + aT;
-    if (col.w >= 0.99f) done = true;  // :129-133
-}
 
 __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
     // :141-142 imageStore(rgba8, col / 255): unorm, round to nearest
@@ -403,6 +428,21 @@ __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
     return packed;
 }
 
+struct SplatRegs {  // one survivor's blend inputs, held by the lane that gathered it
+    float mx, my, a, b, c, o, r, g, bl, thr;
+};
+
+// order this wave's LDS writes before its later LDS reads (single-wave workgroup)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float rl(float x, int src) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), src));
+}
+
 template <bool FAST_EXP, bool STATS, int Q>
 __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals, const float2 *__restrict__ m2d,
@@ -410,10 +450,11 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
                                              const float4 *__restrict__ colour, uint32_t *__restrict__ out,
                                              unsigned long long *__restrict__ stats) {
     constexpr int kChunk = Q * 64;
-    __shared__ float4 s_p0[kCap];  // mx, my, conic.x, conic.y
-    __shared__ float4 s_p1[kCap];  // conic.z, opacity, r, g
-    __shared__ float2 s_p2[kCap];  // b, pre-exp skip threshold
-
+    constexpr uint32_t kNone = 0xffffffffu;
+    __shared__ float4 s_col[256];    // pixel state, pixel id = 4*lane + slot
+    __shared__ uint32_t s_done[64];  // per lane: one done byte per slot
+    __shared__ float s_epow[256];    // one survivor's blend events: power
+    __shared__ uint8_t s_epix[256];  //                              pixel id
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     const int xcd = L & 7, kk = L >> 3;
@@ -438,107 +479,169 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
         const int chunks = (end - start + 1023) / 1024;
         end = min(P.E, start + chunks * 1024);
     }
-    float4 c00 = make_float4(0.f, 0.f, 0.f, 0.f), c10 = c00, c01 = c00, c11 = c00;
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    s_done[lane] = (d00 ? 1u : 0u) | (d10 ? 0x100u : 0u) | (d01 ? 0x10000u : 0u) | (d11 ? 0x1000000u : 0u);
+    const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
 
-    uint32_t v[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        const int j = start + q * 64 + lane;
-        v[q] = (j < end) ? vals[j] : 0xffffffffu;
-    }
-    for (int base = start; base < end; base += kChunk) {
-        bool keep[Q];
+    auto load_idx = [&](int base, uint32_t (&v)[Q]) {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            keep[q] = false;
-            if (v[q] != 0xffffffffu) {
-                if (P.no_cull) {
-                    keep[q] = true;
-                } else {
-                    const float4 b = cullbox[v[q]];
-                    keep[q] = (b.x <= bx1) && (b.y >= bx0) && (b.z <= by1) && (b.w >= by0);
-                }
+            const int j = base + q * 64 + lane;
+            v[q] = (j < end) ? vals[j] : kNone;
+        }
+    };
+    auto load_box = [&](const uint32_t (&v)[Q], float4 (&bx)[Q]) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            bx[q] = (v[q] != kNone && !P.no_cull) ? cullbox[v[q]] : make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
+    };
+    auto test = [&](const uint32_t (&v)[Q], const float4 (&bx)[Q], uint64_t (&keep)[Q]) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q)
+            keep[q] = __ballot(v[q] != kNone && (bx[q].x <= bx1) && (bx[q].y >= bx0) && (bx[q].z <= by1) &&
+                               (bx[q].w >= by0));
+    };
+    auto load_data = [&](const uint32_t (&v)[Q], const uint64_t (&keep)[Q], SplatRegs (&d)[Q]) {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            if ((keep[q] >> lane) & 1ull) {
+                const float2 m = m2d[v[q]];
+                const float4 co = conic[v[q]];
+                const float4 cl = colour[v[q]];
+                d[q] = SplatRegs{m.x, m.y, co.x, co.y, co.z, co.w, cl.x, cl.y, cl.z,
+                                 -logf(255.0f * co.w) - 1.0e-3f};
             }
         }
-        uint32_t vn[Q];  // prefetch the next iteration's entry indices
+    };
+
+    // pipeline prologue: A = step being blended, B = next (data in flight), C = boxes in
+    // flight, D = indices in flight
+    uint32_t vA[Q], vB[Q], vC[Q], vD[Q];
+    float4 boxB[Q], boxC[Q];
+    uint64_t keepA[Q], keepB[Q];
+    SplatRegs dA[Q], dB[Q];
+    load_idx(start, vA);
+    load_idx(start + kChunk, vB);
+    load_box(vA, boxB);  // boxes of A (named B's slot for reuse)
+    test(vA, boxB, keepA);
+    load_data(vA, keepA, dA);
+    load_box(vB, boxB);
+    load_idx(start + 2 * kChunk, vC);
+
+    bool all_done = __all(d00 && d10 && d01 && d11);
+    for (int base = start; base < end && !all_done; base += kChunk) {
+        // next step's survivors, then keep its splat data, the boxes after it and the
+        // indices after those in flight while this step blends
+        test(vB, boxB, keepB);
+        load_data(vB, keepB, dB);
+        load_box(vC, boxC);
+        load_idx(base + 3 * kChunk, vD);
+        if (STATS) ++st_iter;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int j = base + kChunk + q * 64 + lane;
-            vn[q] = (j < end) ? vals[j] : 0xffffffffu;
-        }
-        // survivors in list order: (q, lane)
-        uint32_t total = 0, myoff[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const uint64_t bal = __ballot(keep[q]);
-            myoff[q] = total + (uint32_t)__popcll(bal & lanemask_lt());
-            total += (uint32_t)__popcll(bal);
-        }
-        if (STATS) {
-            ++st_iter;
-            st_surv += total;
-        }
-        for (uint32_t r0 = 0; r0 < total; r0 += kCap) {
-            __syncthreads();  // one-wave workgroup: orders LDS reuse (cheap)
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                if (keep[q] && myoff[q] >= r0 && myoff[q] < r0 + kCap) {
-                    const uint32_t pos = myoff[q] - r0;
-                    const float2 m = m2d[v[q]];
-                    const float4 co = conic[v[q]];
-                    const float4 col = colour[v[q]];
-                    s_p0[pos] = make_float4(m.x, m.y, co.x, co.y);
-                    s_p1[pos] = make_float4(co.z, co.w, col.x, col.y);
-                    s_p2[pos] = make_float2(col.z, -logf(255.0f * co.w) - 1.0e-3f);
-                }
-            }
-            __syncthreads();
-            const uint32_t cnt = min((uint32_t)kCap, total - r0);
-            for (uint32_t k = 0; k < cnt; ++k) {
-                if (d00 && d10 && d01 && d11) break;
-                const float4 a = s_p0[k];
-                const float4 b = s_p1[k];
-                const float2 c = s_p2[k];
+            uint64_t mask = keepA[q];
+            if (STATS) st_surv += __popcll(mask);
+            while (mask && !all_done) {
+                const int src = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const float mx = rl(dA[q].mx, src), my = rl(dA[q].my, src);
+                const float ca = rl(dA[q].a, src), cbv = rl(dA[q].b, src), cc = rl(dA[q].c, src);
+                const float thr = rl(dA[q].thr, src);
                 // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
-                const float dx0 = fx0 - a.x, dx1 = fx1 - a.x, dy0 = fy0 - a.y, dy1 = fy1 - a.y;
-                const float ax0 = a.z * dx0 * dx0, ax1 = a.z * dx1 * dx1;
-                const float cy0 = b.x * dy0 * dy0, cy1 = b.x * dy1 * dy1;
-                const float bx0d = a.w * dx0, bx1d = a.w * dx1;
+                const float dx0 = fx0 - mx, dx1 = fx1 - mx, dy0 = fy0 - my, dy1 = fy1 - my;
+                const float ax0 = ca * dx0 * dx0, ax1 = ca * dx1 * dx1;
+                const float cy0 = cc * dy0 * dy0, cy1 = cc * dy1 * dy1;
+                const float bx0d = cbv * dx0, bx1d = cbv * dx1;
                 const float p00 = -0.5f * (ax0 + cy0) - bx0d * dy0;
                 const float p10 = -0.5f * (ax1 + cy0) - bx1d * dy0;
                 const float p01 = -0.5f * (ax0 + cy1) - bx0d * dy1;
                 const float p11 = -0.5f * (ax1 + cy1) - bx1d * dy1;
                 // :118-126 (power > 0 -> continue), plus the exact pre-exp skip
-                const bool n00 = !d00 && !(p00 > 0.0f) && !(p00 < c.y);
-                const bool n10 = !d10 && !(p10 > 0.0f) && !(p10 < c.y);
-                const bool n01 = !d01 && !(p01 > 0.0f) && !(p01 < c.y);
-                const bool n11 = !d11 && !(p11 > 0.0f) && !(p11 < c.y);
+                const bool n00 = !d00 && !(p00 > 0.0f) && !(p00 < thr);
+                const bool n10 = !d10 && !(p10 > 0.0f) && !(p10 < thr);
+                const bool n01 = !d01 && !(p01 > 0.0f) && !(p01 < thr);
+                const bool n11 = !d11 && !(p11 > 0.0f) && !(p11 < thr);
+                const uint64_t b0 = __ballot(n00), b1 = __ballot(n10), b2 = __ballot(n01), b3 = __ballot(n11);
+                const uint32_t e0 = (uint32_t)__popcll(b0), e1 = (uint32_t)__popcll(b1);
+                const uint32_t e2 = (uint32_t)__popcll(b2), e3 = (uint32_t)__popcll(b3);
+                const uint32_t nev = e0 + e1 + e2 + e3;
                 if (STATS) {
-                    const uint64_t bn = __ballot(n00 || n10 || n01 || n11);
                     ++st_kit;
-                    st_anyneed += bn ? 1 : 0;
-                    st_pxneed += __popcll(__ballot(n00)) + __popcll(__ballot(n10)) + __popcll(__ballot(n01)) +
-                                 __popcll(__ballot(n11));
+                    st_anyneed += nev ? 1 : 0;
+                    st_pxneed += nev;
                 }
-                if (n00 || n10 || n01 || n11) {
-                    if (n00) blend_px<FAST_EXP>(p00, b.y, b.z, b.w, c.x, c00, d00);
-                    if (n10) blend_px<FAST_EXP>(p10, b.y, b.z, b.w, c.x, c10, d10);
-                    if (n01) blend_px<FAST_EXP>(p01, b.y, b.z, b.w, c.x, c01, d01);
-                    if (n11) blend_px<FAST_EXP>(p11, b.y, b.z, b.w, c.x, c11, d11);
+                if (nev == 0) continue;  // uniform
+                // compact this survivor's blend events; each pixel occurs at most once, so the
+                // events are independent and may be processed in any order
+                if (n00) {
+                    const uint32_t e = (uint32_t)__popcll(b0 & lt);
+                    s_epix[e] = (uint8_t)(4 * lane + 0);
+                    s_epow[e] = p00;
                 }
+                if (n10) {
+                    const uint32_t e = e0 + (uint32_t)__popcll(b1 & lt);
+                    s_epix[e] = (uint8_t)(4 * lane + 1);
+                    s_epow[e] = p10;
+                }
+                if (n01) {
+                    const uint32_t e = e0 + e1 + (uint32_t)__popcll(b2 & lt);
+                    s_epix[e] = (uint8_t)(4 * lane + 2);
+                    s_epow[e] = p01;
+                }
+                if (n11) {
+                    const uint32_t e = e0 + e1 + e2 + (uint32_t)__popcll(b3 & lt);
+                    s_epix[e] = (uint8_t)(4 * lane + 3);
+                    s_epow[e] = p11;
+                }
+                wave_lds_sync();
+                const float o = rl(dA[q].o, src);
+                const float r = rl(dA[q].r, src), g = rl(dA[q].g, src), bl = rl(dA[q].bl, src);
+                for (uint32_t e = lane; e < nev; e += 64) {
+                    const uint32_t pix = s_epix[e];
+                    const float power = s_epow[e];
+                    const float ex = FAST_EXP ? __expf(power) : exp_defined(power);
+                    const float alpha = fminf(0.99f, ex * o);
+                    if (alpha < 1.0f / 255.0f) continue;
+                    // alphaBlend :59-67
+                    float4 col = s_col[pix];
+                    const float remaining = 1.0f - col.w;
+                    const float aT = alpha * remaining;
+                    col.x = col.x + r * aT;
+                    col.y = col.y + g * aT;
+                    col.z = col.z + bl * aT;
+                    col.w = col.w + aT;
+                    s_col[pix] = col;
+                    if (col.w >= 0.99f) reinterpret_cast<uint8_t *>(s_done)[pix] = 1;  // :129-133
+                }
+                wave_lds_sync();
+                const uint32_t dm = s_done[lane];
+                d00 = (dm & 0xffu) != 0;
+                d10 = (dm & 0xff00u) != 0;
+                d01 = (dm & 0xff0000u) != 0;
+                d11 = (dm & 0xff000000u) != 0;
+                all_done = __all(d00 && d10 && d01 && d11);  // every pixel saturated
             }
         }
+        // rotate the pipeline
 #pragma unroll
-        for (int q = 0; q < Q; ++q) v[q] = vn[q];
-        if (__all(d00 && d10 && d01 && d11)) break;  // every pixel saturated: nothing can change
+        for (int q = 0; q < Q; ++q) {
+            vA[q] = vB[q];
+            vB[q] = vC[q];
+            vC[q] = vD[q];
+            boxB[q] = boxC[q];
+            keepA[q] = keepB[q];
+            dA[q] = dB[q];
+        }
     }
-    if (in00) out[(size_t)pya * P.W + pxa] = pack_rgba8(c00);
-    if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(c10);
-    if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(c01);
-    if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(c11);
+    wave_lds_sync();
+    if (in00) out[(size_t)pya * P.W + pxa] = pack_rgba8(s_col[4 * lane + 0]);
+    if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 1]);
+    if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(s_col[4 * lane + 2]);
+    if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 3]);
     if (STATS && lane == 0) {
         const unsigned long long cyc = __builtin_amdgcn_s_memtime() - st_t0;
         atomicAdd(&stats[0], 1ull);
@@ -557,8 +660,10 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
 
 }  // namespace
 
+int preprocess_blocks(int n) { return (n + kSplatsPerBlock - 1) / kSplatsPerBlock; }
+
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr) {
-    const int nb = (P.n + kBlock - 1) / kBlock;
+    const int nb = preprocess_blocks(P.n);
     if (nb > 0) hipLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kBlock), 0, s, P, sc, fr);
 }
 
@@ -567,7 +672,7 @@ void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks) {
 }
 
 void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals) {
-    const int nb = (n + kBlock - 1) / kBlock;
+    const int nb = preprocess_blocks(n);
     if (nb > 0) hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kBlock), 0, s, n, fr, keys, vals);
 }
 
@@ -589,8 +694,8 @@ void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32
 #define GS_DRAW_Q(F, S)                  \
     do {                                 \
         if (P.q == 2) GS_DRAW(F, S, 2);  \
-        else if (P.q == 8) GS_DRAW(F, S, 8); \
-        else GS_DRAW(F, S, 4);           \
+        else if (P.q == 4) GS_DRAW(F, S, 4); \
+        else GS_DRAW(F, S, 1);           \
     } while (0)
     if (stats) {
         if (fast_exp) GS_DRAW_Q(true, true);
