@@ -1,0 +1,38 @@
+"""Build profiles/pmc_summary.json from rocprofv3 --pmc runs (FETCH_SIZE and WRITE_SIZE in
+separate passes, as MI355X_MICROARCH.md prescribes).
+
+FETCH_SIZE/WRITE_SIZE are in KiB per dispatch.  gfx950 correction: FETCH_SIZE counts 128-B
+streaming requests at 64 B (reads 1/2 of a wide coalesced stream), so for kernels whose reads
+are wide coalesced streams the fetch is doubled; the blend's reads are 4-16-B random gathers
+(64-B requests, counted exactly), so its fetch is used as-is.  Both numbers are recorded.
+usage: python tools/pmc_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv out.json
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+GATHER_KERNELS = {"k_draw"}  # reads are random gathers: FETCH_SIZE taken as exact
+
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for path in sys.argv[1:3]:
+    for x in csv.DictReader(open(path)):
+        m = re.search(r"(k_\w+|__amd_\w+)", x["Kernel_Name"])
+        n = m.group(1) if m else x["Kernel_Name"][:40]
+        acc[n][x["Counter_Name"]].append(float(x["Counter_Value"]))
+out = {}
+for k, cs in acc.items():
+    f = cs.get("FETCH_SIZE", [])
+    w = cs.get("WRITE_SIZE", [])
+    if not f or not w:
+        continue
+    fetch = sum(f) / len(f) * 1024.0
+    write = sum(w) / len(w) * 1024.0
+    corr = 1.0 if k in GATHER_KERNELS else 2.0
+    out[k] = {"dispatches": len(f), "fetch_size_bytes_raw": fetch, "write_size_bytes": write,
+              "fetch_correction": corr, "hbm_bytes_per_launch": fetch * corr + write}
+json.dump(out, open(sys.argv[3], "w"), indent=1, sort_keys=True)
+for k, v in sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
+    print(f"{k:24s} {v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch  (fetch raw {v['fetch_size_bytes_raw'] / 1e6:.1f} "
+          f"x{v['fetch_correction']:.0f}, write {v['write_size_bytes'] / 1e6:.1f})")
