@@ -416,13 +416,19 @@ class Splats:
         check(lib().gs_preprocess(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, ctypes.byref(self.stats)),
               self.ctx.handle)
         self.numDuplicates = int(self.stats.duplicates)
+        self._sorted = False
 
     # src/Splats.cpp:346-354
     def sort(self):
+        if getattr(self, "_sorted", False):
+            return  # already sorted this frame (computeBins ran first)
         check(lib().gs_sort(self.ctx.handle), self.ctx.handle)
+        self._sorted = True
 
-    # src/Splats.cpp:481-512
+    # src/Splats.cpp:481-512.  Tile ranges come from the sorted entries, so with the
+    # reference's call order (computeBins before sort, src/Splats.cpp:593-594) sort runs first.
     def computeBins(self):
+        self.sort()
         check(lib().gs_compute_bins(self.ctx.handle), self.ctx.handle)
 
     # src/Splats.cpp:356-381

@@ -144,8 +144,8 @@ def test_stage_api_matches_gpuRender(ctx, golden_dir):
     z = np.load(os.path.join(golden_dir, "golden_c2.npz"))
     assert np.array_equal(a, z["ref_image"])
     sp.preprocess(*args)
+    sp.computeBins()  # the reference's order: bins, then sort (src/Splats.cpp:593-594)
     sp.sort()
-    sp.computeBins()
     sp.draw(512, 512, 512 / 16.0, 512 / 16.0)
     assert np.array_equal(a, sp.texture())
     assert np.array_equal(np.flipud(a), sp.display())
