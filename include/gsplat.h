@@ -38,6 +38,7 @@ extern "C" {
 #define GS_FLAG_TIMING 4u    /* record per-stage hipEvent timings into gs_frame_stats */
 #define GS_FLAG_NO_CULL 8u   /* disable the (exactness-preserving) per-block entry cull */
 #define GS_FLAG_DRAW_STATS 16u /* count blend work (see gs_draw_stats); slower, diagnostics only */
+#define GS_FLAG_DIAG_NOBLEND 32u /* diagnostics only: the blend streams and culls but does not blend */
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;

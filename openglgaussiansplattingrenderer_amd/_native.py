@@ -23,6 +23,7 @@ GS_FLAG_FAST_EXP = 2
 GS_FLAG_TIMING = 4
 GS_FLAG_NO_CULL = 8
 GS_FLAG_DRAW_STATS = 16
+GS_FLAG_DIAG_NOBLEND = 32
 
 GS_READ_KEYS = 1
 GS_READ_VALS = 2

@@ -455,6 +455,7 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     P.clean = clean ? 1 : 0;
     P.no_cull = (flags & GS_FLAG_NO_CULL) ? 1 : 0;
     P.q = ctx->draw_q;
+    P.diag_noblend = (flags & GS_FLAG_DIAG_NOBLEND) ? 1 : 0;
     // Q9: the reference dispatches (W/32) x (H/32) workgroups of 32x32 pixels
     const int coverW = clean ? width : (width / 32) * 32;
     const int coverH = clean ? height : (height / 32) * 32;

@@ -47,7 +47,8 @@ struct DrawParams {
     int32_t clean;
     int32_t no_cull;
     int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
-    int32_t q;                  // list entries per lane per iteration (2, 4, 8)
+    int32_t q;                  // list entries per lane per pipeline step (1, 2, 4)
+    int32_t diag_noblend;       // diagnostics: skip blending (GS_FLAG_DIAG_NOBLEND)
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };

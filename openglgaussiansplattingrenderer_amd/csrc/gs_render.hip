@@ -428,6 +428,37 @@ __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
     return packed;
 }
 
+// Exact block cull for a survivor of the box test.  Pixels of the sub-block need the splat
+// only where the computed power >= thr, i.e. q = a dx^2 + 2b dx dy + c dy^2 <= -2*thr.  The
+// minimum of the convex quadratic q over the continuous rectangle [x0,x1]x[y0,y1] (a lower
+// bound over its integer pixels) is 0 if the centre is inside, else it lies on an edge:
+// minimise the 1-D quadratic along each edge (clamped).  The splat is dropped only when that
+// minimum exceeds the threshold by margins far above the rounding of power (relative error
+// <= ~6 eps * cond; conics with cond >= 1e4 are never dropped here).
+__device__ __forceinline__ bool ellipse_misses_rect(float mx, float my, float a, float b, float c, float thr,
+                                                    float x0, float x1, float y0, float y1) {
+    const float lim = -2.0f * thr;  // pixels with q <= lim may blend
+    if (!(lim > 0.0f)) return thr > 0.0f;  // thr > 0: no power <= 0 reaches it; NaN / 0: keep
+    const float det = a * c - b * b, tr = a + c;
+    if (!(a > 0.0f && c > 0.0f && det > 0.0f && tr * tr < 1.0e4f * det)) return false;
+    const float X0 = x0 - mx, X1 = x1 - mx, Y0 = y0 - my, Y1 = y1 - my;
+    if (X0 <= 0.0f && X1 >= 0.0f && Y0 <= 0.0f && Y1 >= 0.0f) return false;  // centre inside
+    float qmin = 3.0e38f;
+    // edges x = X0, X1: dy* = -b dx / c clamped to [Y0, Y1]
+    for (int e = 0; e < 2; ++e) {
+        const float dx = e ? X1 : X0;
+        const float dy = fminf(fmaxf(-b * dx / c, Y0), Y1);
+        qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
+    }
+    // edges y = Y0, Y1: dx* = -b dy / a clamped to [X0, X1]
+    for (int e = 0; e < 2; ++e) {
+        const float dy = e ? Y1 : Y0;
+        const float dx = fminf(fmaxf(-b * dy / a, X0), X1);
+        qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
+    }
+    return qmin > lim * 1.002f + 1.0e-3f;
+}
+
 struct SplatRegs {  // one survivor's blend inputs, held by the lane that gathered it
     float mx, my, a, b, c, o, r, g, bl, thr;
 };
@@ -517,6 +548,17 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
             }
         }
     };
+    // exact cull of the survivors whose data has arrived (ballot: uniform keep masks)
+    auto refine = [&](uint64_t (&keep)[Q], const SplatRegs (&d)[Q]) {
+        if (P.no_cull) return;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const bool mine = (keep[q] >> lane) & 1ull;
+            const bool miss = mine && ellipse_misses_rect(d[q].mx, d[q].my, d[q].a, d[q].b, d[q].c, d[q].thr, bx0,
+                                                          bx1, by0, by1);
+            keep[q] &= ~__ballot(miss);
+        }
+    };
 
     // pipeline prologue: A = step being blended, B = next (data in flight), C = boxes in
     // flight, D = indices in flight
@@ -541,6 +583,23 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
         load_box(vC, boxC);
         load_idx(base + 3 * kChunk, vD);
         if (STATS) ++st_iter;
+        refine(keepA, dA);
+        if (P.diag_noblend) {  // diagnostics: stream and cull only (pixels are wrong)
+            if (STATS) {
+#pragma unroll
+                for (int q = 0; q < Q; ++q) st_surv += __popcll(keepA[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                vA[q] = vB[q];
+                vB[q] = vC[q];
+                vC[q] = vD[q];
+                boxB[q] = boxC[q];
+                keepA[q] = keepB[q];
+                dA[q] = dB[q];
+            }
+            continue;
+        }
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             uint64_t mask = keepA[q];

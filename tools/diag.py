@@ -20,7 +20,7 @@ print(f"scene up in {time.time() - t:.1f}s", flush=True)
 u = g.main_camera(W, H).uniforms()
 from openglgaussiansplattingrenderer_amd._native import GS_PARAM_DRAW_Q  # noqa: E402
 variants = [("ref", 0, 1), ("ref+fast", g.GS_FLAG_FAST_EXP, 1), ("clean", g.GS_FLAG_CLEAN, 1),
-            ("clean+fast", g.GS_FLAG_CLEAN | g.GS_FLAG_FAST_EXP, 1), ("ref q2", 0, 2), ("ref q4", 0, 4)]
+            ("clean+fast", g.GS_FLAG_CLEAN | g.GS_FLAG_FAST_EXP, 1), ("ref q2", 0, 2), ("noblend", 32, 1), ("noblend q2", 32, 2), ("nocull", 8, 1)]
 for name, fl, q in variants:
     ctx.set_param(GS_PARAM_DRAW_Q, q)
     sp.flags = fl | g.GS_FLAG_DRAW_STATS
