@@ -38,7 +38,6 @@ extern "C" {
 #define GS_FLAG_TIMING 4u    /* record per-stage hipEvent timings into gs_frame_stats */
 #define GS_FLAG_NO_CULL 8u   /* disable the (exactness-preserving) per-block entry cull */
 #define GS_FLAG_DRAW_STATS 16u /* count blend work (see gs_draw_stats); slower, diagnostics only */
-#define GS_FLAG_DIAG_NOBLEND 32u /* diagnostics only: the blend streams and culls but does not blend */
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -185,16 +184,17 @@ typedef struct gs_timing {
     double ms_frame;       /* first to last event of the frame (includes the E readback gap) */
 } gs_timing;
 int gs_timing_reset(gs_ctx *ctx);
-/* tuning knobs (results never depend on them) */
-#define GS_PARAM_DRAW_Q 1     /* blend: list entries per lane per pipeline step, 1 / 2 / 4 */
-int gs_set_param(gs_ctx *ctx, int param, int value);
 
 /* blend work counters accumulated by GS_FLAG_DRAW_STATS frames: [0] sub-blocks drawn,
  * [1] chunk iterations, [2] entries that survived the block cull, [3] list entries in range,
  * [4] max iterations of one block, [5] max survivors of one block, [6] max / [7] summed
- * block duration in s_memtime cycles, [8] (wave, survivor) steps, [9] steps where some pixel
+ * block duration in s_memrealtime ticks (100 MHz), [8] (wave, survivor) steps, [9] steps where some pixel
  * of the wave needs the exp/blend path, [10] (pixel, survivor) pairs needing it */
 int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset);
+/* per-block trace of the last GS_FLAG_DRAW_STATS draw, 4 uint32 per block in launch order:
+ * start, end (s_memrealtime ticks, 100 MHz, low 32 bits), iterations, survivors.  Returns the
+ * number of blocks copied (<= max_blocks, <= 65536). */
+int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks);
 int gs_timing_read(gs_ctx *ctx, gs_timing *out);
 
 #ifdef __cplusplus

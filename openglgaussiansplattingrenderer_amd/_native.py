@@ -23,7 +23,6 @@ GS_FLAG_FAST_EXP = 2
 GS_FLAG_TIMING = 4
 GS_FLAG_NO_CULL = 8
 GS_FLAG_DRAW_STATS = 16
-GS_FLAG_DIAG_NOBLEND = 32
 
 GS_READ_KEYS = 1
 GS_READ_VALS = 2
@@ -32,7 +31,6 @@ GS_READ_MEANS2D = 4
 GS_READ_CONICS = 5
 GS_READ_CULLBOX = 6
 
-GS_PARAM_DRAW_Q = 1
 
 GS_KERNEL_DRAW = 1
 GS_KERNEL_SORT = 2
@@ -133,7 +131,7 @@ SIGNATURES = {
     "gs_last_kernel_ms": (_i, [_vp, _i, _fp]),
     "gs_timing_reset": (_i, [_vp]),
     "gs_draw_stats": (_i, [_vp, _vp, _i]),
-    "gs_set_param": (_i, [_vp, _i, _i]),
+    "gs_draw_block_trace": (_i, [_vp, _vp, _i]),
     "gs_timing_read": (_i, [_vp, ctypes.POINTER(gs_timing)]),
 }
 

@@ -20,8 +20,7 @@ struct gs_ctx {
 
     // per-splat frame buffers (sized by the largest scene rendered so far)
     int n_cap = 0;
-    float2 *m2d = nullptr;
-    float4 *conic = nullptr;
+    gs::SplatDraw *sd = nullptr;
     float4 *cullbox = nullptr;
     int4 *rec = nullptr;
     uint2 *blocksum = nullptr;
@@ -46,7 +45,6 @@ struct gs_ctx {
     int n = 0;
     int64_t V = 0, D = 0, E = 0;
     uint32_t flags = 0;
-    int draw_q = 1;  // tuning knob (gs_set_param)
     // timing: two event sets (frame parity) so frame f-1's events are read after frame f's
     // mid-frame sync without an extra stall; evs = standalone sort calls
     hipEvent_t ev[2][kEv] = {};
@@ -104,7 +102,7 @@ int ensure_splats(gs_ctx *ctx, int n) {
     const int cap = n;
     const int nb = gs::preprocess_blocks(cap);
     int rc;
-    if ((rc = grow(ctx, ctx->m2d, cap)) || (rc = grow(ctx, ctx->conic, cap)) || (rc = grow(ctx, ctx->cullbox, cap)) ||
+    if ((rc = grow(ctx, ctx->sd, cap)) || (rc = grow(ctx, ctx->cullbox, cap)) ||
         (rc = grow(ctx, ctx->rec, cap)) || (rc = grow(ctx, ctx->blocksum, nb)))
         return rc;
     ctx->n_cap = cap;
@@ -122,8 +120,7 @@ int ensure_entries(gs_ctx *ctx, int64_t e) {
 
 gs::FrameDev frame_dev(gs_ctx *ctx) {
     gs::FrameDev f;
-    f.m2d = ctx->m2d;
-    f.conic = ctx->conic;
+    f.sd = ctx->sd;
     f.cullbox = ctx->cullbox;
     f.rec = ctx->rec;
     f.blocksum = ctx->blocksum;
@@ -202,7 +199,8 @@ int gs_ctx_create(int device, gs_ctx **out) {
         return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
     if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess ||
-        hipMalloc(&ctx->draw_stats, 128) != hipSuccess || hipMemset(ctx->draw_stats, 0, 128) != hipSuccess)
+        hipMalloc(&ctx->draw_stats, gs::kDrawStatsBytes) != hipSuccess ||
+        hipMemset(ctx->draw_stats, 0, gs::kDrawStatsBytes) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
     for (auto &set : ctx->ev)
         for (auto &e : set)
@@ -217,7 +215,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void *bufs[] = {ctx->m2d, ctx->conic, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
+    void *bufs[] = {ctx->sd, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
                     ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
@@ -454,8 +452,6 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     P.E = (int32_t)ctx->E;
     P.clean = clean ? 1 : 0;
     P.no_cull = (flags & GS_FLAG_NO_CULL) ? 1 : 0;
-    P.q = ctx->draw_q;
-    P.diag_noblend = (flags & GS_FLAG_DIAG_NOBLEND) ? 1 : 0;
     // Q9: the reference dispatches (W/32) x (H/32) workgroups of 32x32 pixels
     const int coverW = clean ? width : (width / 32) * 32;
     const int coverH = clean ? height : (height / 32) * 32;
@@ -540,8 +536,20 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     case GS_READ_BINS:
         if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");
         src = ctx->bins; avail = 256; break;
-    case GS_READ_MEANS2D: src = ctx->m2d; avail = 2 * (size_t)ctx->n; break;
-    case GS_READ_CONICS: src = ctx->conic; avail = 4 * (size_t)ctx->n; break;
+    case GS_READ_MEANS2D:
+    case GS_READ_CONICS: {  // fields of the 32-byte blend records
+        const size_t comps = what == GS_READ_MEANS2D ? 2 : 4, off = what == GS_READ_MEANS2D ? 0 : 8;
+        if (count > comps * (size_t)ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");
+        const size_t rows = (count + comps - 1) / comps;
+        if (rows) {
+            std::vector<float> tmp(rows * comps);
+            GS_HIP(ctx, hipMemcpy2DAsync(tmp.data(), comps * 4, (const char *)ctx->sd + off, sizeof(gs::SplatDraw),
+                                         comps * 4, rows, hipMemcpyDeviceToHost, ctx->stream));
+            GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            std::memcpy(host_dst, tmp.data(), count * 4);
+        }
+        return GS_OK;
+    }
     case GS_READ_CULLBOX: src = ctx->cullbox; avail = 4 * (size_t)ctx->n; break;
     default: return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: unknown buffer");
     }
@@ -588,22 +596,21 @@ int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
     return GS_OK;
 }
 
-int gs_set_param(gs_ctx *ctx, int param, int value) {
-    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (param == GS_PARAM_DRAW_Q) {
-        if (value != 1 && value != 2 && value != 4) return set_error(ctx, GS_ERR_INVALID, "draw_q must be 1, 2 or 4");
-        ctx->draw_q = value;
-        return GS_OK;
-    }
-    return set_error(ctx, GS_ERR_INVALID, "unknown parameter");
-}
-
 int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset) {
     if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
     GS_HIP(ctx, hipMemcpyAsync(out, ctx->draw_stats, 128, hipMemcpyDeviceToHost, ctx->stream));
-    if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, 128, ctx->stream));
+    if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, gs::kDrawStatsBytes, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return GS_OK;
+}
+
+int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks) {
+    if (!ctx || !out || max_blocks < 0) return set_error(ctx, GS_ERR_INVALID, "bad argument");
+    const int n = std::min(max_blocks, gs::kDrawTraceBlocks);
+    GS_HIP(ctx, hipMemcpyAsync(out, (const char *)ctx->draw_stats + 128, (size_t)n * 16, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return n;
 }
 
 int gs_timing_reset(gs_ctx *ctx) {

@@ -47,8 +47,6 @@ struct DrawParams {
     int32_t clean;
     int32_t no_cull;
     int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
-    int32_t q;                  // list entries per lane per pipeline step (1, 2, 4)
-    int32_t diag_noblend;       // diagnostics: skip blending (GS_FLAG_DIAG_NOBLEND)
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };
@@ -77,9 +75,15 @@ struct SceneDev {
     const float *opacity;
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
 };
+// per-splat blend inputs, one 32-byte aligned record (the blend gathers it with the colour)
+struct alignas(32) SplatDraw {
+    float mx, my;      // screen position (preprocess.glsl:91-94)
+    float a, b, c, o;  // conic (:134-136) and opacity
+    float thr;         // pre-exp skip threshold -ln(255 o) - 1e-3
+    float pad;
+};
 struct FrameDev {
-    float2 *m2d;
-    float4 *conic;     // conic.xyz, opacity
+    SplatDraw *sd;
     float4 *cullbox;   // conservative pixel box of the alpha >= 1/255 region
     int4 *rec;         // z01 bits, tileX, tileY (-1: no entries), packed rect
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
@@ -90,6 +94,11 @@ void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, co
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks);
 void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals);
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins);
+// GS_FLAG_DRAW_STATS buffer: 16 counters, then per block {start, end} (s_memrealtime, 100 MHz),
+// iterations, survivors
+constexpr int kDrawTraceBlocks = 65536;
+constexpr size_t kDrawStatsBytes = 128 + (size_t)kDrawTraceBlocks * 16;
+
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
                  const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats);
 

@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace gs {
 
 namespace {
@@ -215,8 +217,10 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
                 }
             }
         } while (false);
-        fr.m2d[i] = m2;
-        fr.conic[i] = co;
+        // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
+        // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends), NaN never skips
+        const float thr = -logf(255.0f * co.w) - 1.0e-3f;
+        fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
         fr.cullbox[i] = box;
         fr.rec[i] = rc;
     }
@@ -443,25 +447,24 @@ __device__ __forceinline__ bool ellipse_misses_rect(float mx, float my, float a,
     if (!(a > 0.0f && c > 0.0f && det > 0.0f && tr * tr < 1.0e4f * det)) return false;
     const float X0 = x0 - mx, X1 = x1 - mx, Y0 = y0 - my, Y1 = y1 - my;
     if (X0 <= 0.0f && X1 >= 0.0f && Y0 <= 0.0f && Y1 >= 0.0f) return false;  // centre inside
+    // edge minimisers via v_rcp (1 ulp): a minimiser off by delta raises q by O(delta^2),
+    // orders of magnitude inside the margins below
+    const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
     float qmin = 3.0e38f;
     // edges x = X0, X1: dy* = -b dx / c clamped to [Y0, Y1]
     for (int e = 0; e < 2; ++e) {
         const float dx = e ? X1 : X0;
-        const float dy = fminf(fmaxf(-b * dx / c, Y0), Y1);
+        const float dy = fminf(fmaxf(-b * dx * rc, Y0), Y1);
         qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
     }
     // edges y = Y0, Y1: dx* = -b dy / a clamped to [X0, X1]
     for (int e = 0; e < 2; ++e) {
         const float dy = e ? Y1 : Y0;
-        const float dx = fminf(fmaxf(-b * dy / a, X0), X1);
+        const float dx = fminf(fmaxf(-b * dy * ra, X0), X1);
         qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
     }
     return qmin > lim * 1.002f + 1.0e-3f;
 }
-
-struct SplatRegs {  // one survivor's blend inputs, held by the lane that gathered it
-    float mx, my, a, b, c, o, r, g, bl, thr;
-};
 
 // order this wave's LDS writes before its later LDS reads (single-wave workgroup)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -474,18 +477,18 @@ __device__ __forceinline__ float rl(float x, int src) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, x), src));
 }
 
-template <bool FAST_EXP, bool STATS, int Q>
+__device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+template <bool FAST_EXP, bool STATS>
 __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
-                                             const uint32_t *__restrict__ vals, const float2 *__restrict__ m2d,
-                                             const float4 *__restrict__ conic, const float4 *__restrict__ cullbox,
-                                             const float4 *__restrict__ colour, uint32_t *__restrict__ out,
-                                             unsigned long long *__restrict__ stats) {
-    constexpr int kChunk = Q * 64;
+                                             const uint32_t *__restrict__ vals,
+                                             const float4 *__restrict__ cullbox,
+                                             const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
+                                             uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
     constexpr uint32_t kNone = 0xffffffffu;
     __shared__ float4 s_col[256];    // pixel state, pixel id = 4*lane + slot
     __shared__ uint32_t s_done[64];  // per lane: one done byte per slot
-    __shared__ float s_epow[256];    // one survivor's blend events: power
-    __shared__ uint8_t s_epix[256];  //                              pixel id
+    __shared__ uint2 s_ev[256];      // one survivor's blend events: {pixel id, power bits}
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     const int xcd = L & 7, kk = L >> 3;
@@ -510,190 +513,155 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
         const int chunks = (end - start + 1023) / 1024;
         end = min(P.E, start + chunks * 1024);
     }
+    // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
 #pragma unroll
     for (int k = 0; k < 4; ++k) s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, 0.f);
     s_done[lane] = (d00 ? 1u : 0u) | (d10 ? 0x100u : 0u) | (d01 ? 0x10000u : 0u) | (d11 ? 0x1000000u : 0u);
-    const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
-    const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memtime() : 0ull;
-
-    auto load_idx = [&](int base, uint32_t (&v)[Q]) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int j = base + q * 64 + lane;
-            v[q] = (j < end) ? vals[j] : kNone;
-        }
-    };
-    auto load_box = [&](const uint32_t (&v)[Q], float4 (&bx)[Q]) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            bx[q] = (v[q] != kNone && !P.no_cull) ? cullbox[v[q]] : make_float4(-1e30f, 1e30f, -1e30f, 1e30f);
-    };
-    auto test = [&](const uint32_t (&v)[Q], const float4 (&bx)[Q], uint64_t (&keep)[Q]) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-            keep[q] = __ballot(v[q] != kNone && (bx[q].x <= bx1) && (bx[q].y >= bx0) && (bx[q].z <= by1) &&
-                               (bx[q].w >= by0));
-    };
-    auto load_data = [&](const uint32_t (&v)[Q], const uint64_t (&keep)[Q], SplatRegs (&d)[Q]) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            if ((keep[q] >> lane) & 1ull) {
-                const float2 m = m2d[v[q]];
-                const float4 co = conic[v[q]];
-                const float4 cl = colour[v[q]];
-                d[q] = SplatRegs{m.x, m.y, co.x, co.y, co.z, co.w, cl.x, cl.y, cl.z,
-                                 -logf(255.0f * co.w) - 1.0e-3f};
-            }
-        }
-    };
-    // exact cull of the survivors whose data has arrived (ballot: uniform keep masks)
-    auto refine = [&](uint64_t (&keep)[Q], const SplatRegs (&d)[Q]) {
-        if (P.no_cull) return;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const bool mine = (keep[q] >> lane) & 1ull;
-            const bool miss = mine && ellipse_misses_rect(d[q].mx, d[q].my, d[q].a, d[q].b, d[q].c, d[q].thr, bx0,
-                                                          bx1, by0, by1);
-            keep[q] &= ~__ballot(miss);
-        }
-    };
-
-    // pipeline prologue: A = step being blended, B = next (data in flight), C = boxes in
-    // flight, D = indices in flight
-    uint32_t vA[Q], vB[Q], vC[Q], vD[Q];
-    float4 boxB[Q], boxC[Q];
-    uint64_t keepA[Q], keepB[Q];
-    SplatRegs dA[Q], dB[Q];
-    load_idx(start, vA);
-    load_idx(start + kChunk, vB);
-    load_box(vA, boxB);  // boxes of A (named B's slot for reuse)
-    test(vA, boxB, keepA);
-    load_data(vA, keepA, dA);
-    load_box(vB, boxB);
-    load_idx(start + 2 * kChunk, vC);
-
+    const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const bool cull = !P.no_cull;
+    const int jmax = max(end - 1, 0);
     bool all_done = __all(d00 && d10 && d01 && d11);
-    for (int base = start; base < end && !all_done; base += kChunk) {
-        // next step's survivors, then keep its splat data, the boxes after it and the
-        // indices after those in flight while this step blends
-        test(vB, boxB, keepB);
-        load_data(vB, keepB, dB);
-        load_box(vC, boxC);
-        load_idx(base + 3 * kChunk, vD);
-        if (STATS) ++st_iter;
-        refine(keepA, dA);
-        if (P.diag_noblend) {  // diagnostics: stream and cull only (pixels are wrong)
+
+    // The list streams through a four-stage pipeline, one 64-entry chunk per step; chunk c:
+    //   step c-3: index load (coalesced)            step c-2: box gather
+    //   step c-1: box test, splat-data gather       step c:   exact cull + blend
+    // Each stage's registers live one step, so two slots (ping-pong, unrolled) hold them.
+    // Every global load is issued with the full exec mask and no branch around it, and no
+    // register with a pending load is ever copied: a load under a divergent branch or such a
+    // copy makes the compiler wait for all outstanding loads (vmcnt is in-order) and the
+    // pipeline collapses to one memory latency per step.
+    uint32_t Vi[2], Vb[2];      // indices: as loaded / riding with the box gather
+    float4 Bx[2];               // boxes
+    uint64_t K[2];              // survivors of the box test (then of the exact cull)
+    SplatDraw Dd[2];            // survivor data (lane-held; other lanes hold copies)
+    float4 Dc[2];               // survivor colour
+
+    auto load_idx = [&](int base, uint32_t &v) {
+        const int j = base + lane;
+        const uint32_t x = vals[min(j, jmax)];
+        v = j < end ? x : kNone;
+    };
+    auto gather_box = [&](uint32_t v, uint32_t &vb, float4 &bx) {
+        vb = v;
+        bx = cullbox[v == kNone ? 0u : v];
+    };
+    auto test_and_gather = [&](uint32_t v, const float4 &bx, uint64_t &keep, SplatDraw &d, float4 &c) {
+        const bool in = v != kNone && (!cull || ((bx.x <= bx1) && (bx.y >= bx0) && (bx.z <= by1) && (bx.w >= by0)));
+        keep = ballot(in);
+        // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
+        const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
+        const uint32_t idx = in ? v : first;
+        d = sd[idx];
+        c = colour[idx];
+    };
+    auto blend = [&](uint64_t keep, const SplatDraw &d, const float4 &c) {
+        // exact cull of the survivors (uniform keep mask)
+        if (cull) keep &= ~ballot(((keep >> lane) & 1ull) &&
+                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, bx0, bx1, by0, by1));
+        if (STATS) st_surv += __popcll(keep);
+        while (keep && !all_done) {
+            const int src = __builtin_ctzll(keep);
+            keep &= keep - 1;
+            const float mx = rl(d.mx, src), my = rl(d.my, src);
+            const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
+            const float thr = rl(d.thr, src);
+            // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
+            const float dx0 = fx0 - mx, dx1 = fx1 - mx, dy0 = fy0 - my, dy1 = fy1 - my;
+            const float ax0 = ca * dx0 * dx0, ax1 = ca * dx1 * dx1;
+            const float cy0 = cc * dy0 * dy0, cy1 = cc * dy1 * dy1;
+            const float bx0d = cbv * dx0, bx1d = cbv * dx1;
+            // a saturated pixel's power is replaced by -inf, which never needs a blend
+            const float ninf = -__builtin_inff();
+            const float p00 = d00 ? ninf : -0.5f * (ax0 + cy0) - bx0d * dy0;
+            const float p10 = d10 ? ninf : -0.5f * (ax1 + cy0) - bx1d * dy0;
+            const float p01 = d01 ? ninf : -0.5f * (ax0 + cy1) - bx0d * dy1;
+            const float p11 = d11 ? ninf : -0.5f * (ax1 + cy1) - bx1d * dy1;
+            // :118-126 (power > 0 -> continue), plus the exact pre-exp skip (power < thr)
+            const bool n00 = !(p00 > 0.0f) && !(p00 < thr);
+            const bool n10 = !(p10 > 0.0f) && !(p10 < thr);
+            const bool n01 = !(p01 > 0.0f) && !(p01 < thr);
+            const bool n11 = !(p11 > 0.0f) && !(p11 < thr);
+            // ballots of the bare compares (a ballot of a combined lane bool costs two VALU)
+            const uint64_t b0 = ballot(!(p00 > 0.0f)) & ballot(!(p00 < thr));
+            const uint64_t b1 = ballot(!(p10 > 0.0f)) & ballot(!(p10 < thr));
+            const uint64_t b2 = ballot(!(p01 > 0.0f)) & ballot(!(p01 < thr));
+            const uint64_t b3 = ballot(!(p11 > 0.0f)) & ballot(!(p11 < thr));
+            const uint32_t e0 = (uint32_t)__popcll(b0), e1 = (uint32_t)__popcll(b1);
+            const uint32_t e2 = (uint32_t)__popcll(b2), e3 = (uint32_t)__popcll(b3);
+            const uint32_t nev = e0 + e1 + e2 + e3;
             if (STATS) {
-#pragma unroll
-                for (int q = 0; q < Q; ++q) st_surv += __popcll(keepA[q]);
+                ++st_kit;
+                st_anyneed += nev ? 1 : 0;
+                st_pxneed += nev;
             }
-#pragma unroll
-            for (int q = 0; q < Q; ++q) {
-                vA[q] = vB[q];
-                vB[q] = vC[q];
-                vC[q] = vD[q];
-                boxB[q] = boxC[q];
-                keepA[q] = keepB[q];
-                dA[q] = dB[q];
+            if (nev == 0) continue;  // uniform
+            // compact this survivor's blend events (slot k's after slots < k, lane order via
+            // v_mbcnt); each pixel occurs at most once, so the events are independent
+            auto below = [&](uint64_t m, uint32_t base0) {
+                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
+            };
+            if (n00) s_ev[below(b0, 0)] = make_uint2(4 * lane + 0, __float_as_uint(p00));
+            if (n10) s_ev[below(b1, e0)] = make_uint2(4 * lane + 1, __float_as_uint(p10));
+            if (n01) s_ev[below(b2, e0 + e1)] = make_uint2(4 * lane + 2, __float_as_uint(p01));
+            if (n11) s_ev[below(b3, e0 + e1 + e2)] = make_uint2(4 * lane + 3, __float_as_uint(p11));
+            wave_lds_sync();
+            const float o = rl(d.o, src);
+            const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
+            for (uint32_t e = lane; e < nev; e += 64) {
+                const uint2 ev = s_ev[e];
+                const uint32_t pix = ev.x;
+                const float power = __uint_as_float(ev.y);
+                const float ex = FAST_EXP ? __expf(power) : exp_defined(power);
+                const float alpha = fminf(0.99f, ex * o);
+                if (alpha < 1.0f / 255.0f) continue;
+                // alphaBlend :59-67
+                float4 col = s_col[pix];
+                const float remaining = 1.0f - col.w;
+                const float aT = alpha * remaining;
+                col.x = col.x + r * aT;
+                col.y = col.y + g * aT;
+                col.z = col.z + bl * aT;
+                col.w = col.w + aT;
+                s_col[pix] = col;
+                if (col.w >= 0.99f) reinterpret_cast<uint8_t *>(s_done)[pix] = 1;  // :129-133
             }
-            continue;
+            wave_lds_sync();
+            const uint32_t dm = s_done[lane];
+            d00 = (dm & 0xffu) != 0;
+            d10 = (dm & 0xff00u) != 0;
+            d01 = (dm & 0xff0000u) != 0;
+            d11 = (dm & 0xff000000u) != 0;
+            all_done = __all(d00 && d10 && d01 && d11);  // every pixel saturated
         }
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            uint64_t mask = keepA[q];
-            if (STATS) st_surv += __popcll(mask);
-            while (mask && !all_done) {
-                const int src = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const float mx = rl(dA[q].mx, src), my = rl(dA[q].my, src);
-                const float ca = rl(dA[q].a, src), cbv = rl(dA[q].b, src), cc = rl(dA[q].c, src);
-                const float thr = rl(dA[q].thr, src);
-                // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
-                const float dx0 = fx0 - mx, dx1 = fx1 - mx, dy0 = fy0 - my, dy1 = fy1 - my;
-                const float ax0 = ca * dx0 * dx0, ax1 = ca * dx1 * dx1;
-                const float cy0 = cc * dy0 * dy0, cy1 = cc * dy1 * dy1;
-                const float bx0d = cbv * dx0, bx1d = cbv * dx1;
-                const float p00 = -0.5f * (ax0 + cy0) - bx0d * dy0;
-                const float p10 = -0.5f * (ax1 + cy0) - bx1d * dy0;
-                const float p01 = -0.5f * (ax0 + cy1) - bx0d * dy1;
-                const float p11 = -0.5f * (ax1 + cy1) - bx1d * dy1;
-                // :118-126 (power > 0 -> continue), plus the exact pre-exp skip
-                const bool n00 = !d00 && !(p00 > 0.0f) && !(p00 < thr);
-                const bool n10 = !d10 && !(p10 > 0.0f) && !(p10 < thr);
-                const bool n01 = !d01 && !(p01 > 0.0f) && !(p01 < thr);
-                const bool n11 = !d11 && !(p11 > 0.0f) && !(p11 < thr);
-                const uint64_t b0 = __ballot(n00), b1 = __ballot(n10), b2 = __ballot(n01), b3 = __ballot(n11);
-                const uint32_t e0 = (uint32_t)__popcll(b0), e1 = (uint32_t)__popcll(b1);
-                const uint32_t e2 = (uint32_t)__popcll(b2), e3 = (uint32_t)__popcll(b3);
-                const uint32_t nev = e0 + e1 + e2 + e3;
-                if (STATS) {
-                    ++st_kit;
-                    st_anyneed += nev ? 1 : 0;
-                    st_pxneed += nev;
-                }
-                if (nev == 0) continue;  // uniform
-                // compact this survivor's blend events; each pixel occurs at most once, so the
-                // events are independent and may be processed in any order
-                if (n00) {
-                    const uint32_t e = (uint32_t)__popcll(b0 & lt);
-                    s_epix[e] = (uint8_t)(4 * lane + 0);
-                    s_epow[e] = p00;
-                }
-                if (n10) {
-                    const uint32_t e = e0 + (uint32_t)__popcll(b1 & lt);
-                    s_epix[e] = (uint8_t)(4 * lane + 1);
-                    s_epow[e] = p10;
-                }
-                if (n01) {
-                    const uint32_t e = e0 + e1 + (uint32_t)__popcll(b2 & lt);
-                    s_epix[e] = (uint8_t)(4 * lane + 2);
-                    s_epow[e] = p01;
-                }
-                if (n11) {
-                    const uint32_t e = e0 + e1 + e2 + (uint32_t)__popcll(b3 & lt);
-                    s_epix[e] = (uint8_t)(4 * lane + 3);
-                    s_epow[e] = p11;
-                }
-                wave_lds_sync();
-                const float o = rl(dA[q].o, src);
-                const float r = rl(dA[q].r, src), g = rl(dA[q].g, src), bl = rl(dA[q].bl, src);
-                for (uint32_t e = lane; e < nev; e += 64) {
-                    const uint32_t pix = s_epix[e];
-                    const float power = s_epow[e];
-                    const float ex = FAST_EXP ? __expf(power) : exp_defined(power);
-                    const float alpha = fminf(0.99f, ex * o);
-                    if (alpha < 1.0f / 255.0f) continue;
-                    // alphaBlend :59-67
-                    float4 col = s_col[pix];
-                    const float remaining = 1.0f - col.w;
-                    const float aT = alpha * remaining;
-                    col.x = col.x + r * aT;
-                    col.y = col.y + g * aT;
-                    col.z = col.z + bl * aT;
-                    col.w = col.w + aT;
-                    s_col[pix] = col;
-                    if (col.w >= 0.99f) reinterpret_cast<uint8_t *>(s_done)[pix] = 1;  // :129-133
-                }
-                wave_lds_sync();
-                const uint32_t dm = s_done[lane];
-                d00 = (dm & 0xffu) != 0;
-                d10 = (dm & 0xff00u) != 0;
-                d01 = (dm & 0xff0000u) != 0;
-                d11 = (dm & 0xff000000u) != 0;
-                all_done = __all(d00 && d10 && d01 && d11);  // every pixel saturated
-            }
-        }
-        // rotate the pipeline
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            vA[q] = vB[q];
-            vB[q] = vC[q];
-            vC[q] = vD[q];
-            boxB[q] = boxC[q];
-            keepA[q] = keepB[q];
-            dA[q] = dB[q];
+    };
+
+    // prologue: chunk 0 box-gathered, chunk 1 index-loaded ... see the stage table above
+    int base = start;
+    if (base < end && !all_done) {  // uniform
+        uint32_t v0;
+        load_idx(base, v0);
+        load_idx(base + 64, Vi[1]);
+        load_idx(base + 128, Vi[0]);
+        gather_box(v0, Vb[0], Bx[0]);
+        test_and_gather(Vb[0], Bx[0], K[0], Dd[0], Dc[0]);   // chunk 0: data in flight
+        gather_box(Vi[1], Vb[1], Bx[1]);                     // chunk 1: box in flight
+        // chunk c's stages use slot c & 1 for data, (c + 1) & 1 for the box and c & 1 for the
+        // index; step c (slot u = c & 1) runs:
+        auto step = [&](auto U) {
+            constexpr int u = decltype(U)::value, w = u ^ 1;
+            load_idx(base + 192, Vi[w]);                           // chunk c+3
+            gather_box(Vi[u], Vb[u], Bx[u]);                       // chunk c+2
+            test_and_gather(Vb[w], Bx[w], K[w], Dd[w], Dc[w]);     // chunk c+1
+            if (STATS) ++st_iter;
+            blend(K[u], Dd[u], Dc[u]);                             // chunk c
+            base += 64;
+            return base < end && !all_done;
+        };
+        for (;;) {
+            if (!step(std::integral_constant<int, 0>{})) break;
+            if (!step(std::integral_constant<int, 1>{})) break;
         }
     }
     wave_lds_sync();
@@ -702,7 +670,14 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(s_col[4 * lane + 2]);
     if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 3]);
     if (STATS && lane == 0) {
-        const unsigned long long cyc = __builtin_amdgcn_s_memtime() - st_t0;
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), cyc = t1 - st_t0;
+        if (L < kDrawTraceBlocks) {
+            uint32_t *tr = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stats) + 128) + 4 * L;
+            tr[0] = (uint32_t)st_t0;
+            tr[1] = (uint32_t)t1;
+            tr[2] = (uint32_t)st_iter;
+            tr[3] = (uint32_t)st_surv;
+        }
         atomicAdd(&stats[0], 1ull);
         atomicAdd(&stats[1], st_iter);
         atomicAdd(&stats[2], st_surv);
@@ -745,25 +720,17 @@ void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *count
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
                  const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats) {
     // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks, XCD-major (see k_draw)
-    const dim3 grid(kTiles * kTiles * P.nbx * P.nby);
     if (P.nbx <= 0 || P.nby <= 0) return;
-#define GS_DRAW(F, S, Q)                                                                                       \
-    hipLaunchKernelGGL((k_draw<F, S, Q>), grid, dim3(64), 0, s, P, bins, vals, fr.m2d, fr.conic, fr.cullbox, \
-                       colour, out, stats)
-#define GS_DRAW_Q(F, S)                  \
-    do {                                 \
-        if (P.q == 2) GS_DRAW(F, S, 2);  \
-        else if (P.q == 4) GS_DRAW(F, S, 4); \
-        else GS_DRAW(F, S, 1);           \
-    } while (0)
+    const dim3 grid(kTiles * kTiles * P.nbx * P.nby);
+#define GS_DRAW(F, S) \
+    hipLaunchKernelGGL((k_draw<F, S>), grid, dim3(64), 0, s, P, bins, vals, fr.cullbox, fr.sd, colour, out, stats)
     if (stats) {
-        if (fast_exp) GS_DRAW_Q(true, true);
-        else GS_DRAW_Q(false, true);
+        if (fast_exp) GS_DRAW(true, true);
+        else GS_DRAW(false, true);
     } else {
-        if (fast_exp) GS_DRAW_Q(true, false);
-        else GS_DRAW_Q(false, false);
+        if (fast_exp) GS_DRAW(true, false);
+        else GS_DRAW(false, false);
     }
-#undef GS_DRAW_Q
 #undef GS_DRAW
 }
 

@@ -54,15 +54,19 @@ class Context:
         check(lib().gs_timing_read(self.handle, ctypes.byref(t)), self.handle)
         return {k: getattr(t, k) for k, _ in N.gs_timing._fields_}
 
-    def set_param(self, param: int, value: int):
-        check(lib().gs_set_param(self.handle, int(param), int(value)), self.handle)
-
     def draw_stats(self, reset: bool = True) -> dict:
         a = np.zeros(16, np.uint64)
         check(lib().gs_draw_stats(self.handle, ptr(a), int(reset)), self.handle)
         return dict(blocks=int(a[0]), iterations=int(a[1]), survivors=int(a[2]), list_entries=int(a[3]),
                     max_iterations=int(a[4]), max_survivors=int(a[5]), max_cycles=int(a[6]), sum_cycles=int(a[7]),
                     wave_steps=int(a[8]), steps_any_need=int(a[9]), pixel_needs=int(a[10]))
+
+    def draw_block_trace(self, blocks: int) -> np.ndarray:
+        """[blocks, 4] uint32: start, end (100 MHz ticks), iterations, survivors per draw block."""
+        a = np.zeros((blocks, 4), np.uint32)
+        n = lib().gs_draw_block_trace(self.handle, ptr(a), int(blocks))
+        check(n, self.handle)
+        return a[:n]
 
     def last_kernel_ms(self, kernel: int) -> float:
         ms = ctypes.c_float()

@@ -18,11 +18,9 @@ t = time.time()
 sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
 print(f"scene up in {time.time() - t:.1f}s", flush=True)
 u = g.main_camera(W, H).uniforms()
-from openglgaussiansplattingrenderer_amd._native import GS_PARAM_DRAW_Q  # noqa: E402
-variants = [("ref", 0, 1), ("ref+fast", g.GS_FLAG_FAST_EXP, 1), ("clean", g.GS_FLAG_CLEAN, 1),
-            ("clean+fast", g.GS_FLAG_CLEAN | g.GS_FLAG_FAST_EXP, 1), ("ref q2", 0, 2), ("noblend", 32, 1), ("noblend q2", 32, 2), ("nocull", 8, 1)]
-for name, fl, q in variants:
-    ctx.set_param(GS_PARAM_DRAW_Q, q)
+variants = [("ref", 0), ("ref+fast", g.GS_FLAG_FAST_EXP), ("clean", g.GS_FLAG_CLEAN),
+            ("clean+fast", g.GS_FLAG_CLEAN | g.GS_FLAG_FAST_EXP), ("nocull", g.GS_FLAG_NO_CULL)]
+for name, fl in variants:
     sp.flags = fl | g.GS_FLAG_DRAW_STATS
     sp.render_uniforms(u)
     ctx.draw_stats(reset=True)
