@@ -29,16 +29,25 @@ constexpr int kRadix = 256;
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 __device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
-// mask of the active lanes whose 8-bit digit equals this lane's (8 ballots)
+// mask of the active lanes whose 8-bit digit equals this lane's (8 ballots).  Per bit:
+// s = the lane's bit sign-extended, m &= ~(ballot ^ s) -- one v_bitop3 per mask half
+// (4 VALU per bit instead of the 6-8 a per-lane select costs).
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
-    uint64_t m = active;
+    uint32_t lo = (uint32_t)active, hi = (uint32_t)(active >> 32);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t bb = __ballot(bit);
-        m &= bit ? bb : ~bb;
+        uint32_t sb = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // v_bfe_i32
+        asm volatile("" : "+v"(sb));  // keep the compare on sb (no shift + compare rewrite)
+        const uint64_t bb = __ballot(sb != 0u);
+        lo &= ~((uint32_t)bb ^ sb);
+        hi &= ~((uint32_t)(bb >> 32) ^ sb);
     }
-    return m;
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// number of set bits of m below this lane (v_mbcnt)
+__device__ __forceinline__ uint32_t count_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
@@ -64,33 +73,40 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave
     return off + inc - v;
 }
 
+constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
+
 __global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
                                                       uint32_t *__restrict__ hist, uint32_t nb) {
-    __shared__ uint32_t s_cnt[kWaves][kRadix];
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
+    // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
+    __shared__ uint32_t s_cnt[kRadix * kRep];
+    for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) s_cnt[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems];
+    if (blockIdx.x * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
+        const uint32_t *p = keys + base;
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t idx = base + k * 64;
-        kk[k] = (idx < n) ? keys[idx] : 0u;
+        for (int k = 0; k < kItems; ++k) kk[k] = p[k * 64];
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t idx = base + k * 64;
+            kk[k] = (idx < n) ? keys[idx] : 0u;
+        }
     }
+    const uint32_t rep = (uint32_t)lane & (kRep - 1);
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
-        const bool valid = idx < n;
-        const uint32_t d = (kk[k] >> shift) & 0xffu;
-        const uint64_t m = match_digit(d, __ballot(valid));
-        if (valid && (m & lanemask_lt()) == 0) s_cnt[wid][d] += (uint32_t)__popcll(m);
+        if (idx < n) atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
     }
     __syncthreads();
     const int d = threadIdx.x;
-    uint32_t tot = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) tot += s_cnt[w][d];
-    hist[(size_t)d * nb + blockIdx.x] = tot;
+    const uint4 c0 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep]);
+    const uint4 c1 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep + 4]);
+    hist[(size_t)d * nb + blockIdx.x] = (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
 }
 
 // one block per digit: exclusive scan of that digit's per-tile counts, row total
@@ -138,23 +154,48 @@ __global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restri
     const uint32_t tile0 = blockIdx.x * (uint32_t)kTile;
     const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems], vv[kItems];
+    if (tile0 + kTile <= n) {  // uniform: full tile, immediate offsets
+        const uint32_t *pk = kin + base, *pv = vin + base;
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t idx = base + k * 64;
-        kk[k] = (idx < n) ? kin[idx] : 0u;
-        vv[k] = (idx < n) ? vin[idx] : 0u;
+        for (int k = 0; k < kItems; ++k) {
+            kk[k] = pk[k * 64];
+            vv[k] = pv[k * 64];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t idx = base + k * 64;
+            kk[k] = (idx < n) ? kin[idx] : 0u;
+            vv[k] = (idx < n) ? vin[idx] : 0u;
+        }
     }
-    uint32_t rank[kItems];
+    // Stable rank of each key among this wave's keys of its digit, in (item, lane) order:
+    //   1. per item, the match mask of equal digits (independent VALU work for all items);
+    //   2. per item, its first lane adds the item's count to the wave's counter with a
+    //      returning LDS atomic -- one wave's LDS operations execute in issue order, so the
+    //      returned value is the count of that digit in the earlier items; all 16 atomics are
+    //      issued back to back (one LDS round trip, not one per item);
+    //   3. peers fetch their leader's returned value (ds_bpermute).
+    uint32_t rank[kItems], lead[kItems], old[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
         const bool valid = idx < n;
         const uint32_t d = (kk[k] >> shift) & 0xffu;
         const uint64_t m = match_digit(d, __ballot(valid));
-        const uint32_t prev = s_cnt[wid][d];
-        rank[k] = prev + (uint32_t)__popcll(m & lanemask_lt());
-        if (valid && (m & lanemask_lt()) == 0) s_cnt[wid][d] = prev + (uint32_t)__popcll(m);
+        rank[k] = count_below(m);
+        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
+        old[k] = valid ? (uint32_t)__popcll(m) : 0u;  // count, replaced by the atomic's result
     }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        if (idx < n && lead[k] == (uint32_t)lane)
+            old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+        rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
     __syncthreads();
     {
         const int d = threadIdx.x;  // one thread per digit
