@@ -291,11 +291,23 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblock
 // positions: mains [0,V) in splat order, duplicates [V, V+D) splat-major with the rect
 // walked y-major / x-minor and the main tile skipped (preprocess.glsl:171-188).  Same
 // striped kPer-per-lane layout as k_preprocess; item order (it, lane) == splat order.
+// Duplicates are written cooperatively: a wave's duplicates are contiguous, lane l writes
+// entries l, l+64, ... of that range (coalesced), finding the owning splat by a binary search
+// over the wave's inclusive duplicate counts in LDS and decoding its place in the rect walk.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
                                                  uint32_t *__restrict__ vals) {
     __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ uint32_t s_incl[kBlock / 64][64];  // per wave: inclusive duplicate counts
+    __shared__ int4 s_rec[kBlock / 64][64];       // per wave: the lanes' preprocess records
     const uint2 off = fr.blocksum[blockIdx.x];
     const uint32_t V = fr.totals[0];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
     uint32_t carry_m = off.x, carry_d = off.y;
 #pragma unroll 1
     for (int it = 0; it < kPer; ++it) {
@@ -316,20 +328,42 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
         const uint32_t pm = block_excl_scan256(n_main, s_wave, &t0);
         const uint32_t pd = block_excl_scan256(n_dup, s_wave, &t1);
         if (has) {
-            const float z = u2f((uint32_t)rc.x);
             // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
             const uint32_t mpos = carry_m + pm;
             const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
-            keys[mpos] = f2u((float)tileIndex + z);
+            keys[mpos] = f2u((float)tileIndex + u2f((uint32_t)rc.x));
             vals[mpos] = (uint32_t)i;
-            uint32_t d = V + carry_d + pd;
-            for (int y = minY; y <= maxY; ++y)
-                for (int x = minX; x <= maxX; ++x) {
-                    if (x == tileX && y == tileY) continue;
-                    keys[d] = f2u((float)(uint32_t)(y * 16 + x) + z);
-                    vals[d] = (uint32_t)i;
-                    ++d;
-                }
+        }
+        // this wave's duplicates: [V + carry_d + pd0, + T)
+        const uint32_t pd0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pd);
+        const uint32_t incl = pd - pd0 + n_dup;
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (T) {  // uniform per wave
+            s_incl[wid][lane] = incl;
+            s_rec[wid][lane] = rc;
+            wave_sync_lds();
+            uint32_t *kd = keys + V + carry_d + pd0;
+            uint32_t *vd = vals + V + carry_d + pd0;
+            const int ibase = blockIdx.x * kSplatsPerBlock + it * kBlock + wid * 64;
+            for (uint32_t e = lane; e < T; e += 64) {
+                int s = 0;  // owner: first lane with incl > e
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (s_incl[wid][s + step - 1] <= e) s += step;
+                const uint32_t q = e - (s ? s_incl[wid][s - 1] : 0u);  // index in the owner's walk
+                const int4 r = s_rec[wid][s];
+                const int rx0 = r.w & 0xff, rx1 = (r.w >> 8) & 0xff, ry0 = (r.w >> 16) & 0xff, ry1 = (r.w >> 24) & 0xff;
+                const int w = rx1 - rx0 + 1;
+                // walk position, skipping the main tile if it lies in the rect
+                const bool mainIn = r.y >= rx0 && r.y <= rx1 && r.z >= ry0 && r.z <= ry1;
+                const uint32_t mpos_walk = (uint32_t)((r.z - ry0) * w + (r.y - rx0));
+                const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
+                const uint32_t dy = k / (uint32_t)w, dx = k - dy * (uint32_t)w;
+                const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
+                kd[e] = f2u((float)tile + u2f((uint32_t)r.x));
+                vd[e] = (uint32_t)(ibase + s);
+            }
+            wave_sync_lds();  // s_incl / s_rec are rewritten by the next item
         }
         carry_m += t0;
         carry_d += t1;
