@@ -61,16 +61,21 @@ __device__ __forceinline__ M3 tr3(const M3 &a) {
     return o;
 }
 
-// exp of draw.glsl:122 -- the same definition the oracle states (Cody-Waite + degree-6
-// polynomial); every operation is an IEEE-exact-rounded one, so CPU == GPU bit for bit.
+// exp of draw.glsl:122 -- the same definition the oracle states (ora_expf: Cody-Waite +
+// degree-6 Horner polynomial, each step one correctly rounded fma); every operation is
+// IEEE-exact, so CPU == GPU bit for bit.
 __device__ __forceinline__ float exp_defined(float x) {
     if (!(x >= -80.0f)) return 0.0f;
     if (x > 80.0f) x = 80.0f;
     const float kf = rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693359375f;
-    r = r - kf * -2.12194440e-4f;
-    const float p = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666672f + r * (0.0416666679f +
-                    r * (0.00833333377f + r * 0.00138888892f)))));
+    float r = __builtin_fmaf(-kf, 0.693359375f, x);
+    r = __builtin_fmaf(-kf, -2.12194440e-4f, r);
+    float t = __builtin_fmaf(0.00138888892f, r, 0.00833333377f);
+    t = __builtin_fmaf(t, r, 0.0416666679f);
+    t = __builtin_fmaf(t, r, 0.166666672f);
+    t = __builtin_fmaf(t, r, 0.5f);
+    t = __builtin_fmaf(t, r, 1.0f);
+    const float p = __builtin_fmaf(t, r, 1.0f);
     const int k = (int)kf;
     return p * u2f((uint32_t)(k + 127) << 23);
 }
@@ -513,6 +518,8 @@ __device__ __forceinline__ float rl(float x, int src) {
 
 __device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <bool FAST_EXP, bool STATS>
 __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
@@ -538,7 +545,7 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     const int pxa = x0 + 2 * (lane & 7), pya = y0 + 2 * (lane >> 3);
     const bool in00 = pxa < x1 && pya < y1, in10 = pxa + 1 < x1 && pya < y1;
     const bool in01 = pxa < x1 && pya + 1 < y1, in11 = pxa + 1 < x1 && pya + 1 < y1;
-    const float fx0 = (float)pxa, fx1 = (float)(pxa + 1), fy0 = (float)pya, fy1 = (float)(pya + 1);
+    const f32x2 fxx = {(float)pxa, (float)(pxa + 1)}, fyy = {(float)pya, (float)(pya + 1)};
     const float bx0 = (float)x0, bx1 = (float)(x1 - 1), by0 = (float)y0, by1 = (float)(y1 - 1);
 
     const int start = (t == 0) ? 0 : (int)bins[t - 1];
@@ -602,16 +609,21 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
             const float thr = rl(d.thr, src);
             // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
-            const float dx0 = fx0 - mx, dx1 = fx1 - mx, dy0 = fy0 - my, dy1 = fy1 - my;
-            const float ax0 = ca * dx0 * dx0, ax1 = ca * dx1 * dx1;
-            const float cy0 = cc * dy0 * dy0, cy1 = cc * dy1 * dy1;
-            const float bx0d = cbv * dx0, bx1d = cbv * dx1;
+            // pairs (x0, x1) and (y0, y1) in packed fp32 (v_pk_*): each element is the same
+            // IEEE op sequence as the scalar formula
+            const f32x2 dx = fxx - f32x2{mx, mx}, dy = fyy - f32x2{my, my};
+            const f32x2 ax = (f32x2{ca, ca} * dx) * dx;  // (a*dx)*dx
+            const f32x2 cy = (f32x2{cc, cc} * dy) * dy;  // (c*dy)*dy
+            const f32x2 bxd = f32x2{cbv, cbv} * dx;      // b*dx
+            const f32x2 h = f32x2{-0.5f, -0.5f};
+            const f32x2 r0 = h * (ax + f32x2{cy.x, cy.x}) - bxd * f32x2{dy.x, dy.x};  // (p00, p10)
+            const f32x2 r1 = h * (ax + f32x2{cy.y, cy.y}) - bxd * f32x2{dy.y, dy.y};  // (p01, p11)
             // a saturated pixel's power is replaced by -inf, which never needs a blend
             const float ninf = -__builtin_inff();
-            const float p00 = d00 ? ninf : -0.5f * (ax0 + cy0) - bx0d * dy0;
-            const float p10 = d10 ? ninf : -0.5f * (ax1 + cy0) - bx1d * dy0;
-            const float p01 = d01 ? ninf : -0.5f * (ax0 + cy1) - bx0d * dy1;
-            const float p11 = d11 ? ninf : -0.5f * (ax1 + cy1) - bx1d * dy1;
+            const float p00 = d00 ? ninf : r0.x;
+            const float p10 = d10 ? ninf : r0.y;
+            const float p01 = d01 ? ninf : r1.x;
+            const float p11 = d11 ? ninf : r1.y;
             // :118-126 (power > 0 -> continue), plus the exact pre-exp skip (power < thr)
             const bool n00 = !(p00 > 0.0f) && !(p00 < thr);
             const bool n10 = !(p10 > 0.0f) && !(p10 < thr);

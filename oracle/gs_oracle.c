@@ -410,17 +410,22 @@ void ora_bins(const uint32_t *keys, int64_t n, uint32_t *bins256)
 
 float ora_expf(float x)
 {
-    /* exp for draw.glsl:122.  GLSL leaves exp's rounding to the implementation; this
-     * restatement fixes one: Cody-Waite reduction (cephes constants) + degree-6
-     * polynomial, ~2 ulp.  Inputs below -80 return 0 (exp(-80)*opacity is far below
-     * the 1/255 cut of draw.glsl:123, so the pixel result cannot depend on them). */
+    /* exp for draw.glsl:122.  GLSL leaves exp's rounding to the implementation (3 + 2|x|
+     * ulp allowed); this restatement fixes one: Cody-Waite reduction (cephes constants) and
+     * a degree-6 Horner polynomial, every step one correctly rounded fmaf (~2 ulp).  The
+     * GPU kernel evaluates the same fma sequence, so the two agree bit for bit.  Inputs
+     * below -80 return 0 (exp(-80)*opacity is far below the 1/255 cut of draw.glsl:123). */
     if (!(x >= -80.0f)) return 0.0f;
     if (x > 80.0f) x = 80.0f;
     const float kf = rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693359375f;
-    r = r - kf * -2.12194440e-4f;
-    const float p = 1.0f + r * (1.0f + r * (0.5f + r * (0.166666672f + r * (0.0416666679f +
-                    r * (0.00833333377f + r * 0.00138888892f)))));
+    float r = fmaf(-kf, 0.693359375f, x);
+    r = fmaf(-kf, -2.12194440e-4f, r);
+    float t = fmaf(0.00138888892f, r, 0.00833333377f);
+    t = fmaf(t, r, 0.0416666679f);
+    t = fmaf(t, r, 0.166666672f);
+    t = fmaf(t, r, 0.5f);
+    t = fmaf(t, r, 1.0f);
+    const float p = fmaf(t, r, 1.0f);
     const int k = (int)kf;
     return p * u2f((uint32_t)(k + 127) << 23);
 }
