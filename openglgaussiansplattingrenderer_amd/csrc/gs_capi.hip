@@ -32,7 +32,7 @@ struct gs_ctx {
     gs::SortScratch sort;
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
-    uint32_t *bins = nullptr;        // [256]
+    uint32_t *bins = nullptr;        // [256] tile ranges + [256] draw dispatch order
     unsigned long long *draw_stats = nullptr;  // [8] GS_FLAG_DRAW_STATS counters
     // output staging (host-destination renders)
     uint32_t *img = nullptr;
@@ -198,7 +198,7 @@ int gs_ctx_create(int device, gs_ctx **out) {
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
     if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 256 * 4) != hipSuccess ||
+        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 512 * 4) != hipSuccess ||
         hipMalloc(&ctx->draw_stats, gs::kDrawStatsBytes) != hipSuccess ||
         hipMemset(ctx->draw_stats, 0, gs::kDrawStatsBytes) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));

@@ -423,12 +423,23 @@ __global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restric
 }
 
 // prefixBins.glsl: inclusive scan of the 256 counts
+// inclusive scan of the tile counts -> bins[0..255] (prefixBins.glsl); also the draw's
+// dispatch order bins[256..511]: tiles by list length, longest first (ties by index), so the
+// longest-running sub-blocks start first and the blend's tail is short (speed only)
 __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict__ counts, uint32_t *__restrict__ bins) {
     __shared__ uint32_t s_wave[kBlock / 64];
+    __shared__ uint32_t s_cnt[256];
     const uint32_t v = counts[threadIdx.x];
+    s_cnt[threadIdx.x] = v;
     uint32_t tot;
-    const uint32_t ex = block_excl_scan256(v, s_wave, &tot);
+    const uint32_t ex = block_excl_scan256(v, s_wave, &tot);  // (contains __syncthreads)
     bins[threadIdx.x] = ex + v;
+    uint32_t rank = 0;
+    for (int u = 0; u < 256; ++u) {
+        const uint32_t c = s_cnt[u];
+        rank += (c > v || (c == v && u < (int)threadIdx.x)) ? 1u : 0u;
+    }
+    bins[256 + rank] = threadIdx.x;
 }
 
 // ---------------------------------------------------------------------- draw
@@ -436,26 +447,26 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict
 // the 2x2 pixel quad at (2*(l%8), 2*(l/8)).  Sub-blocks never straddle coarse tiles, so
 // each pixel blends exactly its own tile's list (Q18 resolved).
 //
-// The tile's sorted list is consumed Q*64 entries per step through a register pipeline, so
-// the gathers of later steps are in flight while the current step blends:
-//   step i:   keep(i+1) = box(i+1) touches the sub-block;  issue splat-data gathers for the
-//             survivors of i+1, box gathers for i+2, index loads for i+3;  then blend the
-//             survivors of step i (their data arrived during step i-1).
+// The tile's sorted list is consumed 64 entries per step through a four-stage register
+// pipeline (index load, box gather, box test + splat-data gather, blend; see k_draw), so
+// the loads of the next three steps are in flight while the current step blends.
 // Survivors are never staged in LDS: each stays in the registers of the lane that gathered
 // it and is broadcast with v_readlane while the wave walks the ballot mask in ascending
 // lane order -- exactly list order.  Per survivor, every lane evaluates power for its four
 // pixels; the pixels that can blend become (pixel, power) events, compacted and processed
 // one per lane on the pixel state kept in LDS (a pixel occurs at most once per survivor,
-// so events never conflict, and each pixel still sees its survivors in list order).  Each pixel's arithmetic is the same sequence of IEEE
-// ops as draw.glsl / the oracle, and both filters only drop work draw.glsl would `continue`
-// past (draw.glsl:118-126):
-//   * box cull: the entry's alpha >= 1/255 region misses the sub-block;
+// so events never conflict, and each pixel still sees its survivors in list order).  Each
+// pixel's arithmetic is the same sequence of IEEE ops as draw.glsl / the oracle, and the
+// filters only drop work draw.glsl would `continue` past (draw.glsl:118-126):
+//   * box cull: the entry's alpha >= 1/255 box misses the sub-block;
+//   * exact cull: the alpha >= 1/255 ellipse misses the sub-block (ellipse_misses_rect);
 //   * pre-exp skip: power < ln(1/(255*o)) - 1e-3 implies alpha < 1/255 for any exp
 //     within a few ulp.
-// Block placement is XCD-aware: workgroups are dealt round-robin over the 8 XCDs (block b
-// and b+8 share one), so linear block id L maps to XCD L % 8 and all sub-blocks of coarse
-// tile t go to XCD t % 8, consecutively, gathering the tile's list through one L2 (speed
-// only; any placement gives the same pixels).
+// Block placement (speed only; any placement gives the same pixels): workgroups are dealt
+// round-robin over the 8 XCDs, so linear block id L runs on XCD L % 8.  Tiles are taken in
+// k_bins_scan's longest-list-first order and the tile of rank r goes to XCD r % 8, its
+// sub-blocks consecutively: each tile's list is gathered through one L2, and the longest
+// sub-blocks start first.
 
 __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
     // :141-142 imageStore(rgba8, col / 255): unorm, round to nearest
@@ -533,7 +544,8 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     const int xcd = L & 7, kk = L >> 3;
-    const int t = xcd + 8 * (kk / nsub);  // coarse tile (t % 8 == xcd)
+    // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
+    const int t = (int)bins[256 + xcd + 8 * (kk / nsub)];
     const int sub = kk - (kk / nsub) * nsub;
     const int tx = t & 15, ty = t >> 4;
     const int sby = sub / P.nbx, sbx = sub - sby * P.nbx;
