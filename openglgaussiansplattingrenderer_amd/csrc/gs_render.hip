@@ -435,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict
     const uint32_t ex = block_excl_scan256(v, s_wave, &tot);  // (contains __syncthreads)
     bins[threadIdx.x] = ex + v;
     uint32_t rank = 0;
+#pragma unroll 32
     for (int u = 0; u < 256; ++u) {
         const uint32_t c = s_cnt[u];
         rank += (c > v || (c == v && u < (int)threadIdx.x)) ? 1u : 0u;
