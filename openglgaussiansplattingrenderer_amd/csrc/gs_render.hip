@@ -538,7 +538,6 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
                                              const float4 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
                                              uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
-    constexpr uint32_t kNone = 0xffffffffu;
     __shared__ float4 s_col[256];    // pixel state, pixel id = 4*lane + slot
     __shared__ uint32_t s_done[64];  // per lane: one done byte per slot
     __shared__ uint2 s_ev[256];      // one survivor's blend events: {pixel id, power bits}
@@ -592,17 +591,19 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     SplatDraw Dd[2];            // survivor data (lane-held; other lanes hold copies)
     float4 Dc[2];               // survivor colour
 
-    auto load_idx = [&](int base, uint32_t &v) {
-        const int j = base + lane;
-        const uint32_t x = vals[min(j, jmax)];
-        v = j < end ? x : kNone;
-    };
+    // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
+    // is used as loaded (a select on it right after the load would wait for the load);
+    // whether an entry is in the list follows from its position (chunk base + lane < end).
+    auto load_idx = [&](int base, uint32_t &v) { v = vals[min(base + lane, jmax)]; };
     auto gather_box = [&](uint32_t v, uint32_t &vb, float4 &bx) {
         vb = v;
-        bx = cullbox[v == kNone ? 0u : v];
+        bx = cullbox[v];
     };
-    auto test_and_gather = [&](uint32_t v, const float4 &bx, uint64_t &keep, SplatDraw &d, float4 &c) {
-        const bool in = v != kNone && (!cull || ((bx.x <= bx1) && (bx.y >= bx0) && (bx.z <= by1) && (bx.w >= by0)));
+    auto test_and_gather = [&](int cbase, uint32_t v, const float4 &bx, uint64_t &keep, SplatDraw &d,
+                               float4 &c) {
+        // bitwise, not short-circuit: no branch around the compares
+        const bool in = (cbase + lane < end) &
+                        (!cull | ((bx.x <= bx1) & (bx.y >= bx0) & (bx.z <= by1) & (bx.w >= by0)));
         keep = ballot(in);
         // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
         const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
         load_idx(base + 64, Vi[1]);
         load_idx(base + 128, Vi[0]);
         gather_box(v0, Vb[0], Bx[0]);
-        test_and_gather(Vb[0], Bx[0], K[0], Dd[0], Dc[0]);   // chunk 0: data in flight
+        test_and_gather(base, Vb[0], Bx[0], K[0], Dd[0], Dc[0]);   // chunk 0: data in flight
         gather_box(Vi[1], Vb[1], Bx[1]);                     // chunk 1: box in flight
         // chunk c's stages use slot c & 1 for data, (c + 1) & 1 for the box and c & 1 for the
         // index; step c (slot u = c & 1) runs:
@@ -712,7 +713,7 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
             constexpr int u = decltype(U)::value, w = u ^ 1;
             load_idx(base + 192, Vi[w]);                           // chunk c+3
             gather_box(Vi[u], Vb[u], Bx[u]);                       // chunk c+2
-            test_and_gather(Vb[w], Bx[w], K[w], Dd[w], Dc[w]);     // chunk c+1
+            test_and_gather(base + 64, Vb[w], Bx[w], K[w], Dd[w], Dc[w]);   // chunk c+1
             if (STATS) ++st_iter;
             blend(K[u], Dd[u], Dc[u]);                             // chunk c
             base += 64;
