@@ -130,9 +130,17 @@ int gs_scene_count(const gs_scene *scene);
 /* ---------------------------------------------------------------- frame
  * Splats::gpuRender (src/Splats.cpp:587-597) = preprocess -> sort -> bins -> draw.
  * out_rgba8: W*H*4 bytes, row y = GL row y (bottom-up as in the reference texture);
- * on the host (out_on_device = 0) or a device pointer (1).  stats may be NULL. */
+ * on the host (out_on_device = 0) or a device pointer (1).  stats may be NULL.
+ * With stats == NULL, a device output and no GS_FLAG_TIMING, the frame is enqueued without
+ * any host round trip (the entry count stays on the device; buffers are sized from the
+ * previous frame's count with headroom).  Such a frame is complete and correct after
+ * gs_sync (or any call that reads results back): a frame whose entries outgrew the buffers
+ * is detected there and rendered again into the same output.  Keep the scene and the output
+ * buffer alive until then. */
 int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
               void *out_rgba8, int out_on_device, gs_frame_stats *stats);
+/* counts (num_splats, visible, duplicates, entries) of the newest frame; waits for it */
+int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats);
 
 /* stage-level entry points mirroring the reference's Splats methods */
 /* Splats::preprocess (src/Splats.cpp:542-585) + the per-splat entry emission.
@@ -184,6 +192,13 @@ typedef struct gs_timing {
     double ms_frame;       /* first to last event of the frame (includes the E readback gap) */
 } gs_timing;
 int gs_timing_reset(gs_ctx *ctx);
+/* which hipEvents a frame records (each event idles the stream a few microseconds):
+ * GS_TIMING_FRAME 0 the frame end only; GS_TIMING_DRAW 1 + the draw kernel (ms_draw);
+ * GS_TIMING_STAGES 2 every stage (default; all gs_timing fields) */
+#define GS_TIMING_FRAME 0
+#define GS_TIMING_DRAW 1
+#define GS_TIMING_STAGES 2
+int gs_timing_enable(gs_ctx *ctx, int mode);
 
 /* blend work counters accumulated by GS_FLAG_DRAW_STATS frames: [0] sub-blocks drawn,
  * [1] chunk iterations, [2] entries that survived the block cull, [3] list entries in range,

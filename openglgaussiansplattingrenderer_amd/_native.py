@@ -27,6 +27,9 @@ GS_FLAG_DRAW_STATS = 16
 GS_READ_KEYS = 1
 GS_READ_VALS = 2
 GS_READ_BINS = 3
+GS_TIMING_FRAME = 0
+GS_TIMING_DRAW = 1
+GS_TIMING_STAGES = 2
 GS_READ_MEANS2D = 4
 GS_READ_CONICS = 5
 GS_READ_CULLBOX = 6
@@ -120,6 +123,7 @@ SIGNATURES = {
     "gs_scene_destroy": (None, [_vp]),
     "gs_scene_count": (_i, [_vp]),
     "gs_render": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, _vp, _i, ctypes.POINTER(gs_frame_stats)]),
+    "gs_last_stats": (_i, [_vp, _vp]),
     "gs_preprocess": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, ctypes.POINTER(gs_frame_stats)]),
     "gs_sort": (_i, [_vp]),
     "gs_compute_bins": (_i, [_vp]),
@@ -130,6 +134,7 @@ SIGNATURES = {
     "gs_pad_buffer": (_i, [_i, _i]),
     "gs_last_kernel_ms": (_i, [_vp, _i, _fp]),
     "gs_timing_reset": (_i, [_vp]),
+    "gs_timing_enable": (_i, [_vp, _i]),
     "gs_draw_stats": (_i, [_vp, _vp, _i]),
     "gs_draw_block_trace": (_i, [_vp, _vp, _i]),
     "gs_timing_read": (_i, [_vp, ctypes.POINTER(gs_timing)]),

@@ -12,6 +12,7 @@
 // frame events: 0 start, 1 preprocess+scan done, 2 emit start, 3 emit done,
 // 4 sort start, 5 sort done, 6 bins done, 7 draw start, 8 draw done
 constexpr int kEv = 9;
+constexpr int kRing = 4;
 
 struct gs_ctx {
     int device = 0;
@@ -25,7 +26,6 @@ struct gs_ctx {
     int4 *rec = nullptr;
     uint2 *blocksum = nullptr;
     uint32_t *totals = nullptr;      // device [4]
-    uint32_t *h_totals = nullptr;    // pinned [4]
     // entries
     int64_t e_cap = 0;
     uint32_t *keys = nullptr, *vals = nullptr;
@@ -43,14 +43,35 @@ struct gs_ctx {
     // frame state
     int stage = 0;  // 0 none, 1 preprocessed, 2 sorted, 3 binned
     int n = 0;
-    int64_t V = 0, D = 0, E = 0;
+    int64_t V = 0, D = 0, E = 0;  // of the newest frame whose counts the host has seen
     uint32_t flags = 0;
-    // timing: two event sets (frame parity) so frame f-1's events are read after frame f's
-    // mid-frame sync without an extra stall; evs = standalone sort calls
-    hipEvent_t ev[2][kEv] = {};
-    hipEvent_t evs[2] = {};
-    int cur = 0;           // event set of the frame in flight
-    bool pending = false;  // a finished frame's events not yet accumulated
+    // Frames in flight.  Each frame takes the next of kRing slots: its hipEvent set, its
+    // pinned (V, D) and -- for a frame enqueued without a host round trip ("speculative":
+    // the entry count stays on the device, kernels are sized by the entry capacity) -- what is
+    // needed to render it again if its entry count turns out to exceed that capacity.
+    // Reusing a slot waits for the frame that held it, kRing frames back (flow control).
+    struct Slot {
+        bool used = false;  // events not yet folded into acc
+        bool spec = false;  // speculative: totals not yet checked against cap
+        uint64_t seq = 0;
+        const gs_scene *scene = nullptr;
+        gs_uniforms u{};
+        uint32_t flags = 0;
+        void *out = nullptr;
+        int64_t cap = 0;
+    };
+    Slot slot[kRing];
+    hipEvent_t ev[kRing][kEv] = {};
+    hipEvent_t evs[2] = {};      // standalone sort calls
+    uint32_t *h_ring = nullptr;      // pinned [kRing][4]: (V, D) of each slot's frame ...
+    uint32_t *h_ring_dev = nullptr;  // ... as the device sees it (written by k_scan_blocksums)
+    // which events a frame records (each costs the stream a few microseconds of idle):
+    // 0 the frame end only, 1 + the draw kernel's start, 2 every stage boundary (default)
+    int timing_mode = 2;
+    uint64_t seq = 0;
+    int cur = 0;                 // slot of the newest frame
+    std::vector<gs_scene *> scenes;  // live scenes (detached when the ctx goes first)
+    bool e_known = false;        // an entry count has been observed (sizes speculative frames)
     gs_timing acc = {};
 };
 
@@ -91,7 +112,10 @@ int use_device(gs_ctx *ctx) {
 
 template <typename T>
 int grow(gs_ctx *ctx, T *&p, size_t count) {
-    if (p) (void)hipFree(p);
+    if (p) {  // frames in flight may still use the old buffer
+        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        (void)hipFree(p);
+    }
     p = nullptr;
     GS_HIP(ctx, hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T)));
     return GS_OK;
@@ -125,6 +149,7 @@ gs::FrameDev frame_dev(gs_ctx *ctx) {
     f.rec = ctx->rec;
     f.blocksum = ctx->blocksum;
     f.totals = ctx->totals;
+    f.h_totals = ctx->h_ring_dev + 4 * ctx->cur;
     return f;
 }
 
@@ -151,17 +176,104 @@ float elapsed(hipEvent_t a, hipEvent_t b) {
 void accumulate(gs_ctx *ctx, int set) {
     hipEvent_t *e = ctx->ev[set];
     ctx->acc.frames += 1;
+    if (ctx->timing_mode >= 1) ctx->acc.ms_draw += elapsed(e[7], e[8]);
+    if (ctx->timing_mode < 2) return;
     ctx->acc.ms_preprocess += elapsed(e[0], e[1]);
     ctx->acc.ms_emit += elapsed(e[2], e[3]);
     ctx->acc.ms_sort += elapsed(e[4], e[5]);
     ctx->acc.ms_bins += elapsed(e[5], e[6]);
-    ctx->acc.ms_draw += elapsed(e[7], e[8]);
     ctx->acc.ms_frame += elapsed(e[0], e[8]);
 }
 
-int rec(gs_ctx *ctx, int i) {
-    GS_HIP(ctx, hipEventRecord(ctx->ev[ctx->cur][i], ctx->stream));
+// event i of the frame in flight, per the timing mode (GS_FLAG_TIMING: all); the frame-end
+// event (kEv - 1, on the draw kernel) always: it retires the slot
+hipEvent_t fev(gs_ctx *ctx, int i) {
+    const int mode = (ctx->flags & GS_FLAG_TIMING) ? 2 : ctx->timing_mode;
+    if (i == kEv - 1 || mode >= 2 || (mode == 1 && i == 7)) return ctx->ev[ctx->cur][i];
+    return nullptr;
+}
+
+int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out,
+                int out_on_device, gs_frame_stats *stats);
+
+int oldest_used(const gs_ctx *ctx, uint64_t seq_limit) {
+    int k = -1;
+    for (int i = 0; i < kRing; ++i)
+        if (ctx->slot[i].used && ctx->slot[i].seq <= seq_limit && (k < 0 || ctx->slot[i].seq < ctx->slot[k].seq))
+            k = i;
+    return k;
+}
+
+// A speculative frame's entries exceeded its capacity (emission dropped the excess, so its
+// image is wrong).  Every frame still in flight is complete after the sync; the speculative
+// ones are the newest (every host-synchronous operation validates first), so grow the entry
+// buffers and render them again, in order, through the synchronous path.
+int handle_overflow(gs_ctx *ctx) {
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    gs_ctx::Slot redo[kRing];
+    int nredo = 0;
+    int64_t need = 0;
+    for (int k; (k = oldest_used(ctx, ~0ull)) >= 0;) {
+        gs_ctx::Slot &sl = ctx->slot[k];
+        if (sl.spec) {
+            redo[nredo++] = sl;
+            need = std::max<int64_t>(need, (int64_t)ctx->h_ring[4 * k] + ctx->h_ring[4 * k + 1]);
+        }
+        sl.used = false;  // the dropped frames' timings are not accumulated
+    }
+    if (int rc = ensure_entries(ctx, need)) return rc;
+    for (int i = 0; i < nredo; ++i)
+        if (int rc = render_sync(ctx, redo[i].scene, &redo[i].u, redo[i].flags, redo[i].out, 1, nullptr)) return rc;
     return GS_OK;
+}
+
+// wait for and retire the frames with seq <= seq_limit, oldest first: check speculative
+// frames' entry counts against their capacity, fold their timings
+int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
+    for (int k; (k = oldest_used(ctx, seq_limit)) >= 0;) {
+        gs_ctx::Slot &sl = ctx->slot[k];
+        GS_HIP(ctx, hipEventSynchronize(ctx->ev[k][kEv - 1]));
+        if (sl.spec) {
+            const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
+            if (V + D > sl.cap) return handle_overflow(ctx);
+            ctx->V = V;
+            ctx->D = D;
+            ctx->E = V + D;
+            ctx->e_known = true;
+        }
+        accumulate(ctx, k);
+        sl.used = false;
+    }
+    return GS_OK;
+}
+
+bool any_spec(const gs_ctx *ctx) {
+    for (const auto &sl : ctx->slot)
+        if (sl.used && sl.spec) return true;
+    return false;
+}
+
+// every frame enqueued so far is complete and correct (and, if it was speculative, its counts
+// are on the host)
+int validate_all(gs_ctx *ctx) {
+    if (!any_spec(ctx)) return GS_OK;
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return retire_upto(ctx, ~0ull);
+}
+
+// take the next slot for a new frame (retiring the frame that held it)
+int begin_frame(gs_ctx *ctx) {
+    for (;;) {
+        const int k = (ctx->cur + 1) % kRing;
+        if (!ctx->slot[k].used) {
+            ctx->cur = k;
+            ctx->slot[k] = gs_ctx::Slot{};
+            ctx->slot[k].used = true;
+            ctx->slot[k].seq = ++ctx->seq;
+            return GS_OK;
+        }
+        if (int rc = retire_upto(ctx, ctx->slot[k].seq)) return rc;
+    }
 }
 
 }  // namespace
@@ -197,16 +309,25 @@ int gs_ctx_create(int device, gs_ctx **out) {
     if ((rc = use_device(ctx))) return fail(rc);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
-    if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_totals, 16, hipHostMallocDefault) != hipSuccess ||
+    if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_ring, 16 * kRing, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 512 * 4) != hipSuccess ||
         hipMalloc(&ctx->draw_stats, gs::kDrawStatsBytes) != hipSuccess ||
         hipMemset(ctx->draw_stats, 0, gs::kDrawStatsBytes) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
+    if (hipHostGetDevicePointer((void **)&ctx->h_ring_dev, ctx->h_ring, 0) != hipSuccess ||
+        hipMemset(ctx->bin_counts, 0, 256 * 4) != hipSuccess)
+        return fail(set_error(nullptr, GS_ERR_HIP, "ctx setup failed"));
+    // stage events are timing-only: no system-scope fence (its cache writeback / invalidate
+    // idles the stream for microseconds); the frame-end event keeps it, since the host reads
+    // the frame's pinned counts after it
     for (auto &set : ctx->ev)
-        for (auto &e : set)
-            if (hipEventCreate(&e) != hipSuccess) return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
+        for (int i = 0; i < kEv; ++i)
+            if (hipEventCreateWithFlags(&set[i], i == kEv - 1 ? hipEventDefault : hipEventDisableSystemFence) !=
+                hipSuccess)
+                return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
     for (auto &e : ctx->evs)
-        if (hipEventCreate(&e) != hipSuccess) return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess)
+            return fail(set_error(nullptr, GS_ERR_HIP, "hipEventCreate failed"));
     *out = ctx;
     return GS_OK;
 }
@@ -215,11 +336,12 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     void *bufs[] = {ctx->sd, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
                     ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    if (ctx->h_totals) (void)hipHostFree(ctx->h_totals);
+    if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
     gs::sort_free(ctx->sort);
     for (auto &set : ctx->ev)
         for (auto &e : set)
@@ -233,7 +355,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
 int gs_sync(gs_ctx *ctx) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    return GS_OK;
+    return validate_all(ctx);  // speculative frames checked (and rendered again if they overflowed)
 }
 
 void *gs_stream(gs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
@@ -246,7 +368,9 @@ int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr) {
 }
 int gs_free(gs_ctx *ctx, void *dptr) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (dptr) GS_HIP(ctx, hipFree(dptr));
+    if (!dptr) return GS_OK;
+    if (int rc = gs_sync(ctx)) return rc;  // frames in flight (or their re-renders) may use it
+    GS_HIP(ctx, hipFree(dptr));
     return GS_OK;
 }
 int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
@@ -257,6 +381,7 @@ int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
 }
 int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (int rc = gs_sync(ctx)) return rc;  // speculative frames complete and checked first
     GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return GS_OK;
@@ -337,13 +462,18 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
     GS_HIP(ctx, hipMemcpyAsync(s->soa, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     if (n > 0) GS_HIP(ctx, hipMemcpyAsync(s->colour, colours4, nn * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->scenes.push_back(s);
     *out = s;
     return GS_OK;
 }
 
 void gs_scene_destroy(gs_scene *scene) {
     if (!scene) return;
-    if (scene->ctx) (void)hipSetDevice(scene->ctx->device);
+    if (gs_ctx *ctx = scene->ctx) {
+        (void)hipSetDevice(ctx->device);
+        (void)gs_sync(ctx);  // frames in flight (and their re-renders) may read the scene
+        ctx->scenes.erase(std::remove(ctx->scenes.begin(), ctx->scenes.end(), scene), ctx->scenes.end());
+    }
     if (scene->soa) (void)hipFree(scene->soa);
     if (scene->colour) (void)hipFree(scene->colour);
     delete scene;
@@ -352,14 +482,11 @@ void gs_scene_destroy(gs_scene *scene) {
 int gs_scene_count(const gs_scene *scene) { return scene ? scene->n : -1; }
 
 // ---------------------------------------------------------------------- frame
-int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, gs_frame_stats *stats) {
-    if (!ctx || !scene || !u) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: null argument");
-    if (scene->ctx != ctx) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: scene belongs to another ctx");
-    if (u->width <= 0 || u->height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: bad resolution");
-    if (int rc = use_device(ctx)) return rc;
-    ctx->flags = flags;
-    const int n = scene->n;
-    if (int rc = ensure_splats(ctx, n)) return rc;
+}  // extern "C"
+
+namespace {
+
+gs::PreParams pre_params(const gs_uniforms *u, uint32_t flags, int n) {
     gs::PreParams P;
     std::memcpy(P.view, u->view, sizeof(P.view));
     std::memcpy(P.vp, u->vp, sizeof(P.vp));
@@ -378,78 +505,62 @@ int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint
         P.tile_h = (float)u->height / 16.f;
     }
     P.n = n;
+    return P;
+}
+
+int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, const char *who) {
+    if (!ctx || !scene || !u) return set_error(ctx, GS_ERR_INVALID, std::string(who) + ": null argument");
+    if (scene->ctx != ctx) return set_error(ctx, GS_ERR_INVALID, std::string(who) + ": scene belongs to another ctx");
+    if (u->width <= 0 || u->height <= 0) return set_error(ctx, GS_ERR_INVALID, std::string(who) + ": bad resolution");
+    return use_device(ctx);
+}
+
+// preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->totals
+int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {
+    const int n = scene->n;
+    if (int rc = ensure_splats(ctx, n)) return rc;
+    if (int rc = begin_frame(ctx)) return rc;
+    ctx->flags = flags;
+    const gs::PreParams P = pre_params(u, flags, n);
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = gs::preprocess_blocks(n);
-    const int prev = ctx->cur;
-    const bool had_pending = ctx->pending;
-    ctx->cur ^= 1;
-    ctx->pending = false;
-    if (int rc = rec(ctx, 0)) return rc;
-    GS_HIP(ctx, hipMemsetAsync(ctx->totals, 0, 16, ctx->stream));
-    gs::launch_preprocess(ctx->stream, P, scene_dev(scene), fr);
-    if (nb > 0) gs::launch_scan_blocksums(ctx->stream, fr, nb);
+    // k_scan_blocksums writes (V, D) to ctx->totals and to this slot's pinned host copy
+    gs::launch_preprocess(ctx->stream, P, scene_dev(scene), fr, fev(ctx, 0));
+    gs::launch_scan_blocksums(ctx->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
     GS_HIP(ctx, hipGetLastError());
-    if (int rc = rec(ctx, 1)) return rc;
-    // E is needed on the host to size the sort (the reference maps its atomic counter back
-    // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
-    GS_HIP(ctx, hipMemcpyAsync(ctx->h_totals, ctx->totals, 8, hipMemcpyDeviceToHost, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (had_pending) accumulate(ctx, prev);  // the previous frame has completed
-    ctx->V = ctx->h_totals[0];
-    ctx->D = ctx->h_totals[1];
-    ctx->E = ctx->V + ctx->D;
-    if (ctx->E >= ((int64_t)1 << 31)) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: more than 2^31 entries");
-    if (int rc = ensure_entries(ctx, ctx->E)) return rc;
-    if (int rc = rec(ctx, 2)) return rc;
-    gs::launch_emit(ctx->stream, n, fr, ctx->keys, ctx->vals);
-    GS_HIP(ctx, hipGetLastError());
-    if (int rc = rec(ctx, 3)) return rc;
     ctx->n = n;
-    ctx->stage = 1;
-    if (stats) {
-        stats->num_splats = n;
-        stats->visible = ctx->V;
-        stats->duplicates = ctx->D;
-        stats->entries = ctx->E;
-    }
     return GS_OK;
 }
 
-int gs_sort(gs_ctx *ctx) {
-    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_sort: call gs_preprocess first");
-    if (int rc = use_device(ctx)) return rc;
-    if (int rc = rec(ctx, 4)) return rc;
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, ctx->E, ctx->err)) return set_error(ctx, rc, ctx->err);
-    if (int rc = rec(ctx, 5)) return rc;
-    ctx->stage = 2;
-    return GS_OK;
-}
-
-int gs_compute_bins(gs_ctx *ctx) {
-    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (ctx->stage < 2) return set_error(ctx, GS_ERR_STATE, "gs_compute_bins: call gs_sort first");
-    if (int rc = use_device(ctx)) return rc;
-    GS_HIP(ctx, hipMemsetAsync(ctx->bin_counts, 0, 256 * 4, ctx->stream));
-    gs::launch_bins(ctx->stream, ctx->keys, ctx->E, ctx->bin_counts, ctx->bins);
+int enqueue_emit(gs_ctx *ctx) {
+    gs::launch_emit(ctx->stream, ctx->n, frame_dev(ctx), ctx->keys, ctx->vals, (uint32_t)ctx->e_cap, fev(ctx, 2),
+                    fev(ctx, 3));
     GS_HIP(ctx, hipGetLastError());
-    if (int rc = rec(ctx, 6)) return rc;
-    ctx->stage = 3;
     return GS_OK;
 }
 
-int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w, float tile_h, uint32_t flags,
-            void *out_rgba8, int out_on_device) {
-    if (!ctx || !scene || !out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_draw: null argument");
-    if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_draw: call gs_compute_bins first");
-    if (width <= 0 || height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_draw: bad resolution");
-    if (scene->n != ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_draw: scene differs from the preprocessed one");
-    if (int rc = use_device(ctx)) return rc;
+// E entries, or (count != null) min(E, count[0] + count[1]) read on the device
+int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count) {
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, E, ctx->err, count, fev(ctx, 4),
+                                fev(ctx, 5)))
+        return set_error(ctx, rc, ctx->err);
+    return GS_OK;
+}
+
+int enqueue_bins(gs_ctx *ctx, int64_t E, const uint32_t *count) {
+    gs::launch_bins(ctx->stream, ctx->keys, E, count, ctx->bin_counts, ctx->bins, fev(ctx, 6));
+    GS_HIP(ctx, hipGetLastError());
+    return GS_OK;
+}
+
+int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w, float tile_h,
+                 uint32_t flags, void *out_rgba8, int out_on_device, int64_t E, const uint32_t *count) {
     const bool clean = (flags & GS_FLAG_CLEAN) != 0;
     gs::DrawParams P;
     P.W = width;
     P.H = height;
-    P.E = (int32_t)ctx->E;
+    P.E = (int32_t)E;
+    P.count = count;
     P.clean = clean ? 1 : 0;
     P.no_cull = (flags & GS_FLAG_NO_CULL) ? 1 : 0;
     // Q9: the reference dispatches (W/32) x (H/32) workgroups of 32x32 pixels
@@ -485,13 +596,12 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
         }
         dst = ctx->img;
     }
-    if (coverW < width || coverH < height) GS_HIP(ctx, hipMemsetAsync(dst, 0, npx * 4, ctx->stream));
-    if (int rc = rec(ctx, 7)) return rc;
-    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), scene->colour,
-                    dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr);
+    P.coverW = coverW;
+    P.coverH = coverH;
+    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx),
+                    scene->colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
+                    fev(ctx, 8));
     GS_HIP(ctx, hipGetLastError());
-    if (int rc = rec(ctx, 8)) return rc;
-    ctx->pending = true;
     if (!out_on_device) {
         GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
         GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -499,17 +609,112 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     return GS_OK;
 }
 
-int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
-              int out_on_device, gs_frame_stats *stats) {
-    if (!ctx || !scene || !u || !out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_render: null argument");
+// the host-synchronous frame: one 8-byte readback of (V, D) sizes the entry buffers
+int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out,
+                int out_on_device, gs_frame_stats *stats) {
     int rc;
     if ((rc = gs_preprocess(ctx, scene, u, flags, stats))) return rc;
     if ((rc = gs_sort(ctx))) return rc;
     if ((rc = gs_compute_bins(ctx))) return rc;
     // src/Splats.cpp:596 draw(width, height, float(width) / 16.f, float(height) / 16.f)
-    if ((rc = gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
-                      out_rgba8, out_on_device)))
+    return gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags, out,
+                   out_on_device);
+}
+
+// the speculative frame: no host round trip.  Kernels after the scan read the entry count on
+// the device and are sized by the entry capacity (last observed count + 25 % + 64Ki); the
+// slot keeps what is needed to render the frame again should the count exceed it.
+int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out) {
+    const int64_t want = std::max<int64_t>(ctx->E + ctx->E / 4 + 65536, (int64_t)scene->n + 4096);
+    if (ctx->e_cap < want)
+        if (int rc = ensure_entries(ctx, want)) return rc;
+    if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
+    gs_ctx::Slot &sl = ctx->slot[ctx->cur];
+    sl.spec = true;
+    sl.scene = scene;
+    sl.u = *u;
+    sl.flags = flags;
+    sl.out = out;
+    sl.cap = ctx->e_cap;
+    const uint32_t *cnt = ctx->totals;
+    int rc;
+    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->e_cap, cnt)) || (rc = enqueue_bins(ctx, ctx->e_cap, cnt)))
         return rc;
+    if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
+                           out, 1, ctx->e_cap, cnt)))
+        return rc;
+    ctx->stage = 3;
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, gs_frame_stats *stats) {
+    if (int rc = check_frame_args(ctx, scene, u, "gs_preprocess")) return rc;
+    if (int rc = validate_all(ctx)) return rc;
+    if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
+    // E is needed on the host to size the sort (the reference maps its atomic counter back
+    // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));  // (V, D) are in the slot's pinned copy
+    ctx->V = ctx->h_ring[4 * ctx->cur];
+    ctx->D = ctx->h_ring[4 * ctx->cur + 1];
+    ctx->E = ctx->V + ctx->D;
+    ctx->e_known = true;
+    if (ctx->E >= ((int64_t)1 << 31)) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: more than 2^31 entries");
+    if (int rc = ensure_entries(ctx, ctx->E)) return rc;
+    if (int rc = enqueue_emit(ctx)) return rc;
+    ctx->stage = 1;
+    if (stats) {
+        stats->num_splats = ctx->n;
+        stats->visible = ctx->V;
+        stats->duplicates = ctx->D;
+        stats->entries = ctx->E;
+    }
+    return GS_OK;
+}
+
+int gs_sort(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (int rc = validate_all(ctx)) return rc;
+    if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_sort: call gs_preprocess first");
+    if (int rc = use_device(ctx)) return rc;
+    if (int rc = enqueue_sort(ctx, ctx->E, nullptr)) return rc;
+    ctx->stage = 2;
+    return GS_OK;
+}
+
+int gs_compute_bins(gs_ctx *ctx) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (int rc = validate_all(ctx)) return rc;
+    if (ctx->stage < 2) return set_error(ctx, GS_ERR_STATE, "gs_compute_bins: call gs_sort first");
+    if (int rc = use_device(ctx)) return rc;
+    if (int rc = enqueue_bins(ctx, ctx->E, nullptr)) return rc;
+    ctx->stage = 3;
+    return GS_OK;
+}
+
+int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w, float tile_h, uint32_t flags,
+            void *out_rgba8, int out_on_device) {
+    if (!ctx || !scene || !out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_draw: null argument");
+    if (int rc = validate_all(ctx)) return rc;
+    if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_draw: call gs_compute_bins first");
+    if (width <= 0 || height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_draw: bad resolution");
+    if (scene->n != ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_draw: scene differs from the preprocessed one");
+    if (int rc = use_device(ctx)) return rc;
+    return enqueue_draw(ctx, scene, width, height, tile_w, tile_h, flags, out_rgba8, out_on_device, ctx->E, nullptr);
+}
+
+int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
+              int out_on_device, gs_frame_stats *stats) {
+    if (!out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_render: null argument");
+    if (int rc = check_frame_args(ctx, scene, u, "gs_render")) return rc;
+    // no stats wanted, output on the device, an entry count seen before: enqueue the whole
+    // frame without a host round trip (validated at gs_sync / the next readback)
+    if (!stats && out_on_device && ctx->e_known && !(flags & GS_FLAG_TIMING))
+        return render_spec(ctx, scene, u, flags, out_rgba8);
+    if (int rc = render_sync(ctx, scene, u, flags, out_rgba8, out_on_device, stats)) return rc;
     if (flags & GS_FLAG_TIMING) {
         hipEvent_t *e = ctx->ev[ctx->cur];
         GS_HIP(ctx, hipEventSynchronize(e[8]));
@@ -524,8 +729,20 @@ int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t
     return GS_OK;
 }
 
+int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats) {
+    if (!ctx || !stats) return set_error(ctx, GS_ERR_INVALID, "gs_last_stats: null argument");
+    if (int rc = gs_sync(ctx)) return rc;
+    *stats = gs_frame_stats{};
+    stats->num_splats = ctx->n;
+    stats->visible = ctx->V;
+    stats->duplicates = ctx->D;
+    stats->entries = ctx->E;
+    return GS_OK;
+}
+
 int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     if (!ctx || (!host_dst && count)) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: null argument");
+    if (int rc = gs_sync(ctx)) return rc;
     if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: no frame");
     if (int rc = use_device(ctx)) return rc;
     const void *src = nullptr;
@@ -570,26 +787,24 @@ int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n
         if (int rc = grow(ctx, ctx->ask, (size_t)n + (size_t)n / 4)) return rc;
         ctx->ask_cap = (size_t)n + (size_t)n / 4;
     }
-    GS_HIP(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-    gs::launch_gather_keys(ctx->stream, d_keys, d_order, ctx->ask, n);
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->ask, (uint32_t *)d_order, n, ctx->err))
+    gs::launch_gather_keys(ctx->stream, d_keys, d_order, ctx->ask, n, ctx->evs[0]);
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->ask, (uint32_t *)d_order, n, ctx->err, nullptr, nullptr,
+                                ctx->evs[1]))
         return set_error(ctx, rc, ctx->err);
-    GS_HIP(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     return GS_OK;
 }
 
 int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n) {
     if (!ctx || (n > 0 && (!d_keys || !d_vals)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_sort_pairs_u32: bad argument");
     if (int rc = use_device(ctx)) return rc;
-    GS_HIP(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, d_keys, d_vals, n, ctx->err)) return set_error(ctx, rc, ctx->err);
-    GS_HIP(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, d_keys, d_vals, n, ctx->err, nullptr, ctx->evs[0], ctx->evs[1]))
+        return set_error(ctx, rc, ctx->err);
     return GS_OK;
 }
 
 int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
     if (!ctx || !ms) return set_error(ctx, GS_ERR_INVALID, "null argument");
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = gs_sync(ctx)) return rc;
     if (kernel == GS_KERNEL_DRAW) *ms = elapsed(ctx->ev[ctx->cur][7], ctx->ev[ctx->cur][8]);
     else if (kernel == GS_KERNEL_SORT) *ms = elapsed(ctx->evs[0], ctx->evs[1]);
     else return set_error(ctx, GS_ERR_INVALID, "unknown kernel");
@@ -613,21 +828,27 @@ int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks) {
     return n;
 }
 
+int gs_timing_enable(gs_ctx *ctx, int mode) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (mode < 0 || mode > 2) return set_error(ctx, GS_ERR_INVALID, "gs_timing_enable: mode must be 0, 1 or 2");
+    if (int rc = gs_sync(ctx)) return rc;
+    if (int rc = retire_upto(ctx, ~0ull)) return rc;
+    ctx->timing_mode = mode;
+    return GS_OK;
+}
+
 int gs_timing_reset(gs_ctx *ctx) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    ctx->pending = false;
+    if (int rc = gs_sync(ctx)) return rc;
+    if (int rc = retire_upto(ctx, ~0ull)) return rc;
     ctx->acc = gs_timing{};
     return GS_OK;
 }
 
 int gs_timing_read(gs_ctx *ctx, gs_timing *out) {
     if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->pending) {
-        accumulate(ctx, ctx->cur);
-        ctx->pending = false;
-    }
+    if (int rc = gs_sync(ctx)) return rc;
+    if (int rc = retire_upto(ctx, ~0ull)) return rc;
     *out = ctx->acc;
     return GS_OK;
 }

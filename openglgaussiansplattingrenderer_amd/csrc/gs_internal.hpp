@@ -43,10 +43,12 @@ struct PreParams {
 // Per-frame parameters of the blend kernel (draw.glsl:38-47)
 struct DrawParams {
     int32_t W, H;
-    int32_t E;
+    int32_t E;                  // entries (or their capacity when count is set)
+    const uint32_t *count;      // device (V, D): E = min(E, V + D), or null
     int32_t clean;
     int32_t no_cull;
     int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
+    int32_t coverW, coverH;     // drawn coverage; pixels outside it are zeroed (Q9)
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };
@@ -61,11 +63,15 @@ struct SortScratch {
     uint32_t *row_total = nullptr; // [256]
 };
 
-int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err);
-int sort_ensure(SortScratch &sc, int64_t n, std::string &err);
+// n elements, or -- when dev_count is given -- min(n, dev_count[0] + dev_count[1]) read on the
+// device (n is then the capacity the grids are sized for)
+int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
+               const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]
-void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n);
+void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n,
+                        hipEvent_t start = nullptr);
 
 // render kernels (gs_render.hip)
 struct SceneDev {
@@ -88,18 +94,25 @@ struct FrameDev {
     int4 *rec;         // z01 bits, tileX, tileY (-1: no entries), packed rect
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
     uint32_t *totals;  // [0]=V [1]=D
+    uint32_t *h_totals;  // mapped pinned host copy of (V, D) for this frame, or null
 };
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
-void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr);
-void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks);
-void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals);
-void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins);
+// start / stop: optional hipEvents recorded on the dispatch packets (stage timing)
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start);
+void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);
+void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+                 hipEvent_t start, hipEvent_t stop);
+// E entries, or min(E, dev_count[0] + dev_count[1]) when dev_count is given; counts must be
+// zero on entry and are left zero
+void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,
+                 uint32_t *bins, hipEvent_t stop);
 // GS_FLAG_DRAW_STATS buffer: 16 counters, then per block {start, end} (s_memrealtime, 100 MHz),
 // iterations, survivors
 constexpr int kDrawTraceBlocks = 65536;
 constexpr size_t kDrawStatsBytes = 128 + (size_t)kDrawTraceBlocks * 16;
 
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats);
+                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats, hipEvent_t start,
+                 hipEvent_t stop);
 
 }  // namespace gs

@@ -13,6 +13,7 @@
 
 #include "gs_internal.hpp"
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -289,6 +290,10 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblock
     if (threadIdx.x == 0) {
         fr.totals[0] = s_carry[0];
         fr.totals[1] = s_carry[1];
+        if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
+            fr.h_totals[0] = s_carry[0];
+            fr.h_totals[1] = s_carry[1];
+        }
     }
 }
 
@@ -305,8 +310,10 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Entries at positions >= cap are not written (a frame enqueued before its entry count is
+// known on the host; the host detects the overflow from the totals and renders again).
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
-                                                 uint32_t *__restrict__ vals) {
+                                                 uint32_t *__restrict__ vals, uint32_t cap) {
     __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ uint32_t s_incl[kBlock / 64][64];  // per wave: inclusive duplicate counts
     __shared__ int4 s_rec[kBlock / 64][64];       // per wave: the lanes' preprocess records
@@ -336,8 +343,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
             const uint32_t mpos = carry_m + pm;
             const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
-            keys[mpos] = f2u((float)tileIndex + u2f((uint32_t)rc.x));
-            vals[mpos] = (uint32_t)i;
+            if (mpos < cap) {
+                keys[mpos] = f2u((float)tileIndex + u2f((uint32_t)rc.x));
+                vals[mpos] = (uint32_t)i;
+            }
         }
         // this wave's duplicates: [V + carry_d + pd0, + T)
         const uint32_t pd0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pd);
@@ -347,8 +356,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             s_incl[wid][lane] = incl;
             s_rec[wid][lane] = rc;
             wave_sync_lds();
-            uint32_t *kd = keys + V + carry_d + pd0;
-            uint32_t *vd = vals + V + carry_d + pd0;
+            const uint32_t d0 = V + carry_d + pd0;
+            const uint32_t room = cap > d0 ? cap - d0 : 0u;  // entries of this range that fit
+            uint32_t *kd = keys + d0;
+            uint32_t *vd = vals + d0;
             const int ibase = blockIdx.x * kSplatsPerBlock + it * kBlock + wid * 64;
             for (uint32_t e = lane; e < T; e += 64) {
                 int s = 0;  // owner: first lane with incl > e
@@ -365,8 +376,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
                 const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
                 const uint32_t dy = k / (uint32_t)w, dx = k - dy * (uint32_t)w;
                 const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
-                kd[e] = f2u((float)tile + u2f((uint32_t)r.x));
-                vd[e] = (uint32_t)(ibase + s);
+                if (e < room) {
+                    kd[e] = f2u((float)tile + u2f((uint32_t)r.x));
+                    vd[e] = (uint32_t)(ibase + s);
+                }
             }
             wave_sync_lds();  // s_incl / s_rec are rewritten by the next item
         }
@@ -379,8 +392,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
 // countBins.glsl: bins[int(key)]++ for int(key) in [0,256).  Keys are already sorted, so
 // each thread run-length counts 16 consecutive keys and flushes a run to LDS on change.
 constexpr int kBinItems = 16;
-__global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restrict__ keys, int64_t E,
+__global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restrict__ keys, int64_t E_max,
+                                                       const uint32_t *__restrict__ cnt,
                                                        uint32_t *__restrict__ counts) {
+    const int64_t E = cnt ? min(E_max, (int64_t)cnt[0] + (int64_t)cnt[1]) : E_max;
     __shared__ uint32_t s_cnt[256];
     s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -423,13 +438,14 @@ __global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restric
 }
 
 // prefixBins.glsl: inclusive scan of the 256 counts
-// inclusive scan of the tile counts -> bins[0..255] (prefixBins.glsl); also the draw's
+// inclusive scan of the tile counts -> bins[0..255] (prefixBins.glsl), counts re-zeroed; also the draw's
 // dispatch order bins[256..511]: tiles by list length, longest first (ties by index), so the
 // longest-running sub-blocks start first and the blend's tail is short (speed only)
-__global__ __launch_bounds__(kBlock) void k_bins_scan(const uint32_t *__restrict__ counts, uint32_t *__restrict__ bins) {
+__global__ __launch_bounds__(kBlock) void k_bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins) {
     __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ uint32_t s_cnt[256];
     const uint32_t v = counts[threadIdx.x];
+    counts[threadIdx.x] = 0;  // ready for the next frame's k_bins_count (no memset launch)
     s_cnt[threadIdx.x] = v;
     uint32_t tot;
     const uint32_t ex = block_excl_scan256(v, s_wave, &tot);  // (contains __syncthreads)
@@ -543,6 +559,28 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     __shared__ uint2 s_ev[256];      // one survivor's blend events: {pixel id, power bits}
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
+    if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
+        // drawn coverage (Q9: the reference dispatches (W/32)x(H/32) groups of 32x32); done here
+        // instead of a memset launch
+        const int rw = P.W - P.coverW, right = rw * P.coverH;
+        const int total = right + (P.H - P.coverH) * P.W;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int m = (L - kTiles * kTiles * nsub) * 256 + k * 64 + (int)threadIdx.x;
+            if (m >= total) break;
+            int x, y;
+            if (m < right) {
+                y = m / rw;
+                x = P.coverW + (m - y * rw);
+            } else {
+                const int q = m - right;
+                y = P.coverH + q / P.W;
+                x = q - (y - P.coverH) * P.W;
+            }
+            out[(size_t)y * P.W + x] = 0u;
+        }
+        return;
+    }
     const int xcd = L & 7, kk = L >> 3;
     // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
     const int t = (int)bins[256 + xcd + 8 * (kk / nsub)];
@@ -563,8 +601,9 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
     const int start = (t == 0) ? 0 : (int)bins[t - 1];
     int end = (int)bins[t];
     if (!P.clean && end > start) {  // Q10: the last 1024-entry chunk is blended whole
+        const int E = P.count ? min(P.E, (int)(P.count[0] + P.count[1])) : P.E;
         const int chunks = (end - start + 1023) / 1024;
-        end = min(P.E, start + chunks * 1024);
+        end = min(E, start + chunks * 1024);
     }
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
@@ -756,34 +795,42 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
 
 int preprocess_blocks(int n) { return (n + kSplatsPerBlock - 1) / kSplatsPerBlock; }
 
-void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr) {
+// Stage timing rides on the dispatch packets (hipExtLaunchKernelGGL start / stop events): a
+// separate hipEventRecord costs an idle gap of several microseconds on the stream.
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start) {
     const int nb = preprocess_blocks(P.n);
-    if (nb > 0) hipLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kBlock), 0, s, P, sc, fr);
+    if (nb > 0) hipExtLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
 }
 
-void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks) {
-    hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, fr, nblocks);
+void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, start, stop, 0, fr, nblocks);
 }
 
-void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals) {
-    const int nb = preprocess_blocks(n);
-    if (nb > 0) hipLaunchKernelGGL(k_emit, dim3(nb), dim3(kBlock), 0, s, n, fr, keys, vals);
+void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+                 hipEvent_t start, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_emit, dim3(std::max(preprocess_blocks(n), 1)), dim3(kBlock), 0, s, start, stop, 0, n, fr,
+                          keys, vals, cap);
 }
 
-void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, uint32_t *counts, uint32_t *bins) {
+void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,
+                 uint32_t *bins, hipEvent_t stop) {
     const int64_t per = (int64_t)kBlock * kBinItems;
     const int64_t nb = (E + per - 1) / per;
-    if (nb > 0) hipLaunchKernelGGL(k_bins_count, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, E, counts);
-    hipLaunchKernelGGL(k_bins_scan, dim3(1), dim3(kBlock), 0, s, counts, bins);
+    if (nb > 0)
+        hipLaunchKernelGGL(k_bins_count, dim3((unsigned)nb), dim3(kBlock), 0, s, keys, E, dev_count, counts);
+    hipExtLaunchKernelGGL(k_bins_scan, dim3(1), dim3(kBlock), 0, s, nullptr, stop, 0, counts, bins);
 }
 
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats) {
-    // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks, XCD-major (see k_draw)
-    if (P.nbx <= 0 || P.nby <= 0) return;
-    const dim3 grid(kTiles * kTiles * P.nbx * P.nby);
-#define GS_DRAW(F, S) \
-    hipLaunchKernelGGL((k_draw<F, S>), grid, dim3(64), 0, s, P, bins, vals, fr.cullbox, fr.sd, colour, out, stats)
+                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats, hipEvent_t start,
+                 hipEvent_t stop) {
+    // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks, XCD-major (see k_draw), then the
+    // margin blocks (256 uncovered pixels each); with no coverage only margin blocks run
+    const int margin = P.W * P.H - P.coverW * P.coverH;
+    const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
+#define GS_DRAW(F, S)                                                                                         \
+    hipExtLaunchKernelGGL((k_draw<F, S>), grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, \
+                          colour, out, stats)
     if (stats) {
         if (fast_exp) GS_DRAW(true, true);
         else GS_DRAW(false, true);

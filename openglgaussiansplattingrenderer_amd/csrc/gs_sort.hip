@@ -13,6 +13,7 @@
 // one the reference's test (tests/sortTests.cpp:240-243) and the oracle define.
 #include "gs_internal.hpp"
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 namespace gs {
@@ -27,7 +28,6 @@ constexpr int kTile = kThreads * kItems;      // 4096
 constexpr int kRadix = 256;
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
-__device__ __forceinline__ uint64_t lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // mask of the active lanes whose 8-bit digit equals this lane's (8 ballots).  Per bit:
 // s = the lane's bit sign-extended, m &= ~(ballot ^ s) -- one v_bitop3 per mask half
@@ -75,8 +75,16 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave
 
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
-__global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n, int shift,
+// element count: n, or min(n, cnt[0] + cnt[1]) when the count lives on the device (a frame
+// enqueued without a host round trip; the grid is sized for n, the capacity)
+__device__ __forceinline__ uint32_t elem_count(uint32_t n, const uint32_t *cnt) {
+    return cnt ? min(n, cnt[0] + cnt[1]) : n;
+}
+
+__global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
+                                                      const uint32_t *__restrict__ cnt, int shift,
                                                       uint32_t *__restrict__ hist, uint32_t nb) {
+    const uint32_t n = elem_count(n_max, cnt);
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
@@ -139,8 +147,11 @@ __global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist,
 
 __global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                         uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                        uint32_t n, int shift, const uint32_t *__restrict__ hist,
-                                                        uint32_t nb, const uint32_t *__restrict__ row_total) {
+                                                        uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
+                                                        const uint32_t *__restrict__ hist, uint32_t nb,
+                                                        const uint32_t *__restrict__ row_total) {
+    const uint32_t n = elem_count(n_max, cnt);
+    if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count
     __shared__ uint32_t s_cnt[kWaves][kRadix];  // running per-wave counts -> per-wave exclusive offsets
     __shared__ uint32_t s_start[kRadix];        // block-local start of each digit
     __shared__ int32_t s_gbase[kRadix];         // global position of local slot 0 of each digit
@@ -223,8 +234,8 @@ __global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restri
         }
     }
     __syncthreads();
-    const uint32_t cnt = min((uint32_t)kTile, n - tile0);
-    for (uint32_t i = threadIdx.x; i < cnt; i += kThreads) {
+    const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
+    for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
         const uint32_t d = (key >> shift) & 0xffu;
         const uint32_t o = (uint32_t)(s_gbase[d] + (int32_t)i);
@@ -241,9 +252,11 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 }  // namespace
 
-int sort_ensure(SortScratch &sc, int64_t n, std::string &err) {
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s) {
     const size_t nb = (size_t)((n + kTile - 1) / kTile);
-    if ((size_t)n > sc.alt_cap) {
+    const bool grow_alt = (size_t)n > sc.alt_cap, grow_hist = nb * kRadix > sc.hist_cap;
+    if ((grow_alt && sc.keys_alt) || (grow_hist && sc.hist)) (void)hipStreamSynchronize(s);  // in-flight users
+    if (grow_alt) {
         if (sc.keys_alt) (void)hipFree(sc.keys_alt);
         if (sc.vals_alt) (void)hipFree(sc.vals_alt);
         sc.keys_alt = sc.vals_alt = nullptr;
@@ -255,7 +268,7 @@ int sort_ensure(SortScratch &sc, int64_t n, std::string &err) {
         }
         sc.alt_cap = cap;
     }
-    if (nb * kRadix > sc.hist_cap) {
+    if (grow_hist) {
         if (sc.hist) (void)hipFree(sc.hist);
         sc.hist = nullptr;
         const size_t cap = (nb + nb / 4 + 16) * kRadix;
@@ -280,22 +293,29 @@ void sort_free(SortScratch &sc) {
     sc = SortScratch{};
 }
 
-int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err) {
-    if (n <= 1) return GS_OK;
+int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
+               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop) {
+    if ((n <= 1 && !dev_count) || n < 1) {  // nothing to sort; the timing events still mark the call
+        if (start) (void)hipEventRecord(start, s);
+        if (stop) (void)hipEventRecord(stop, s);
+        return GS_OK;
+    }
     if (n >= (int64_t)1 << 31) {
         err = "radix sort: n must be < 2^31";
         return GS_ERR_INVALID;
     }
-    int rc = sort_ensure(sc, n, err);
+    int rc = sort_ensure(sc, n, err, s);
     if (rc) return rc;
     const uint32_t nb = (uint32_t)((n + kTile - 1) / kTile);
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
-        hipLaunchKernelGGL(k_upsweep, dim3(nb), dim3(kThreads), 0, s, kin, (uint32_t)n, shift, sc.hist, nb);
+        // timing events on the first and last dispatch (see launch_preprocess)
+        hipExtLaunchKernelGGL(k_upsweep, dim3(nb), dim3(kThreads), 0, s, pass == 0 ? start : nullptr, nullptr, 0, kin,
+                              (uint32_t)n, dev_count, shift, sc.hist, nb);
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, sc.row_total);
-        hipLaunchKernelGGL(k_downsweep, dim3(nb), dim3(kThreads), 0, s, kin, vin, kout, vout, (uint32_t)n, shift,
-                           sc.hist, nb, sc.row_total);
+        hipExtLaunchKernelGGL(k_downsweep, dim3(nb), dim3(kThreads), 0, s, nullptr, pass == 3 ? stop : nullptr, 0, kin,
+                              vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
@@ -307,9 +327,14 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     return GS_OK;
 }
 
-void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n) {
+void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n,
+                        hipEvent_t start) {
     const int64_t nb = (n + 255) / 256;
-    if (nb > 0) hipLaunchKernelGGL(k_gather_keys, dim3((unsigned)nb), dim3(256), 0, s, keys, order, kout, n);
+    if (nb > 0)
+        hipExtLaunchKernelGGL(k_gather_keys, dim3((unsigned)nb), dim3(256), 0, s, start, nullptr, 0, keys, order, kout,
+                              n);
+    else if (start)
+        (void)hipEventRecord(start, s);
 }
 
 }  // namespace gs

@@ -54,6 +54,10 @@ class Context:
         check(lib().gs_timing_read(self.handle, ctypes.byref(t)), self.handle)
         return {k: getattr(t, k) for k, _ in N.gs_timing._fields_}
 
+    def timing_enable(self, mode: int):
+        """GS_TIMING_FRAME / GS_TIMING_DRAW / GS_TIMING_STAGES (gs_timing_enable)"""
+        check(lib().gs_timing_enable(self.handle, int(mode)), self.handle)
+
     def draw_stats(self, reset: bool = True) -> dict:
         a = np.zeros(16, np.uint64)
         check(lib().gs_draw_stats(self.handle, ptr(a), int(reset)), self.handle)
@@ -360,7 +364,6 @@ class Splats:
             self.means3D, self.colours, self.opacities, self.scales, self.rotations = arrays
             self.numSplats = len(self.means3D)
         self.sphericalHarmonics = np.zeros(0, np.float32)  # never filled (include/Splats.h:59)
-        self.numDuplicates = 0
         self.computeCovarianceMatrices()
         self._scene = None
         self.loadToGPU(width, height)
@@ -401,12 +404,24 @@ class Splats:
         self._scene = h
         self.width, self.height = int(width), int(height)
         self._texture = DeviceBuffer(self.ctx, self.width * self.height * 4)
-        self.stats = N.gs_frame_stats()
+        self._stats = N.gs_frame_stats()
+
+    @property
+    def stats(self) -> N.gs_frame_stats:
+        """counts of the newest frame (gs_last_stats: waits for it)"""
+        st = N.gs_frame_stats()
+        check(lib().gs_last_stats(self.ctx.handle, ctypes.byref(st)), self.ctx.handle)
+        return st
+
+    @property
+    def numDuplicates(self) -> int:
+        """include/Splats.h:56 -- duplicate entries of the newest frame"""
+        return int(self.stats.duplicates)
 
     def __del__(self):
         try:
             if self._scene is not None:
-                lib().gs_scene_destroy(self._scene)
+                lib().gs_scene_destroy(self._scene)  # safe after the ctx is gone (detached)
                 self._scene = None
         except Exception:
             pass
@@ -417,9 +432,8 @@ class Splats:
         self._preprocess_u(u)
 
     def _preprocess_u(self, u: N.gs_uniforms):
-        check(lib().gs_preprocess(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, ctypes.byref(self.stats)),
+        check(lib().gs_preprocess(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, ctypes.byref(self._stats)),
               self.ctx.handle)
-        self.numDuplicates = int(self.stats.duplicates)
         self._sorted = False
 
     # src/Splats.cpp:346-354
@@ -452,9 +466,9 @@ class Splats:
         if u.width * u.height * 4 > self._texture.nbytes:
             self._texture = DeviceBuffer(self.ctx, u.width * u.height * 4)
         self.width, self.height = int(u.width), int(u.height)
-        check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, self._texture.ptr, 1,
-                              ctypes.byref(self.stats)), self.ctx.handle)
-        self.numDuplicates = int(self.stats.duplicates)
+        # no stats pointer: the frame is enqueued without a host round trip (gs_render)
+        check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, self._texture.ptr, 1, None),
+              self.ctx.handle)
 
     def texture(self) -> np.ndarray:
         """RGBA8 image (H, W, 4); row 0 = GL row 0 (bottom of the screen)."""

@@ -1,0 +1,106 @@
+"""Frames enqueued without a host round trip (gs_render with no stats and a device output):
+the entry count stays on the device and the buffers are sized from the previous count.
+These frames must give exactly the pixels of the host-synchronous path, including when
+the entries outgrow the buffers (detected at gs_sync and rendered again)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import openglgaussiansplattingrenderer_amd as g
+from openglgaussiansplattingrenderer_amd import _native as N
+from openglgaussiansplattingrenderer_amd._native import check, lib
+from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+
+pytestmark = pytest.mark.gpu
+
+
+def make_splats(ctx, n, seed, W, H):
+    rng = np.random.default_rng(seed)
+    means = rng.uniform(-2, 2, (n, 3)).astype(np.float32)
+    rot = rng.normal(size=(n, 4)).astype(np.float32)
+    rot /= np.linalg.norm(rot, axis=1, keepdims=True)
+    sc = np.exp(rng.uniform(np.log(0.01), np.log(0.2), (n, 3))).astype(np.float32)
+    op = rng.uniform(0.05, 0.99, n).astype(np.float32)
+    col = rng.normal(size=(n, 3)).astype(np.float32)
+    return g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+
+
+def render_sync(sp, u, out):
+    """gs_render with a stats pointer: the host-synchronous path"""
+    st = N.gs_frame_stats()
+    check(lib().gs_render(sp.ctx.handle, sp._scene, ctypes.byref(u), sp.flags, out.ptr, 1, ctypes.byref(st)),
+          sp.ctx.handle)
+    return st
+
+
+def render_spec(sp, u, out):
+    check(lib().gs_render(sp.ctx.handle, sp._scene, ctypes.byref(u), sp.flags, out.ptr, 1, None), sp.ctx.handle)
+
+
+def pose(W, H, k):
+    cam = g.main_camera(W, H)
+    cam.rotateRight(8.0 * k)  # every pose k < 7 still sees the scene
+    return cam.uniforms()
+
+
+@pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
+def test_frames_in_flight_match_sync(flags):
+    W, H = 512, 384
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx, flags=flags)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(6)]
+    render_sync(sp, pose(W, H, 0), outs[0])  # first frame on the ctx: counts seen once
+    for k in range(6):  # six frames back to back, more than the 4 slots in flight
+        render_spec(sp, pose(W, H, k), outs[k])
+    ctx.sync()
+    got = [o.download(np.uint8, W * H * 4) for o in outs]
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    for k in range(6):
+        st = render_sync(sp, pose(W, H, k), ref)
+        assert np.array_equal(got[k], ref.download(np.uint8, W * H * 4)), f"pose {k}"
+        assert st.entries > 0
+    ctx.close()
+
+
+def test_overflow_renders_again():
+    W, H = 640, 480
+    ctx = g.Context(0)
+    small = make_splats(ctx, 500, 1, W, H)
+    big = make_splats(ctx, 200_000, 2, W, H)
+    out_s = g.DeviceBuffer(ctx, W * H * 4)
+    out_b = g.DeviceBuffer(ctx, W * H * 4)
+    u = pose(W, H, 0)
+    st_small = render_sync(small, u, out_s)  # sizes the buffers for ~500 splats
+    render_spec(big, u, out_b)  # far more entries than that capacity
+    ctx.sync()  # detects the overflow and renders the frame again
+    got = out_b.download(np.uint8, W * H * 4)
+    st = big.stats
+    assert st.entries > 4 * (st_small.entries + st_small.entries // 4 + 65536), "the case must overflow"
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    st_ref = render_sync(big, u, ref)
+    assert st.entries == st_ref.entries and st.visible == st_ref.visible
+    assert np.array_equal(got, ref.download(np.uint8, W * H * 4))
+    ctx.close()
+
+
+def test_staged_calls_after_inflight_frames():
+    """the stage API validates frames in flight first (counts on the host, results intact)"""
+    W, H = 256, 256
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    u = pose(W, H, 1)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, u, out)
+    render_spec(sp, u, out)
+    E = int(sp.stats.entries)
+    keys = sp.read(g.GS_READ_KEYS, E)
+    assert np.all(np.diff(keys.astype(np.int64)) >= 0)
+    sp._preprocess_u(u)
+    sp.computeBins()
+    sp.draw(W, H, W / 16.0, H / 16.0)
+    img = sp.texture().reshape(-1)
+    assert np.array_equal(img, out.download(np.uint8, W * H * 4))
+    ctx.close()

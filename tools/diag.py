@@ -29,12 +29,17 @@ for name, fl in variants:
     sp.flags = fl
     for _ in range(3):
         sp.render_uniforms(u)
+    ctx.timing_enable(g.GS_TIMING_DRAW)  # wall time as bench.py measures it
     ctx.timing_reset()
     t0 = time.perf_counter()
     for _ in range(frames):
         sp.render_uniforms(u)
     ctx.sync()
     dt = (time.perf_counter() - t0) / frames * 1e3
+    ctx.timing_enable(g.GS_TIMING_STAGES)  # stage breakdown from a second pass
+    ctx.timing_reset()
+    for _ in range(frames):
+        sp.render_uniforms(u)
     tm = ctx.timing_read()
     nf = tm["frames"]
     s = " ".join(f"{k[3:]}={tm[k] / nf:.3f}" for k in ("ms_preprocess", "ms_emit", "ms_sort", "ms_bins", "ms_draw"))
