@@ -85,6 +85,7 @@ __global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ cnt, int shift,
                                                       uint32_t *__restrict__ hist, uint32_t nb) {
     const uint32_t n = elem_count(n_max, cnt);
+    if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count (never scanned)
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
@@ -117,12 +118,15 @@ __global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict
     hist[(size_t)d * nb + blockIdx.x] = (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
 }
 
-// one block per digit: exclusive scan of that digit's per-tile counts, row total
-__global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb,
+// one block per digit: exclusive scan of that digit's per-tile counts (the tiles holding
+// elements; rows are nb long), row total
+__global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
+                                                    const uint32_t *__restrict__ cnt,
                                                     uint32_t *__restrict__ row_total) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
-    uint32_t *row = hist + (size_t)blockIdx.x * nb;
+    const uint32_t nb = (elem_count(n_max, cnt) + kTile - 1) / kTile;
+    uint32_t *row = hist + (size_t)blockIdx.x * nb_stride;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry = 0;
     __syncthreads();
@@ -313,7 +317,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         // timing events on the first and last dispatch (see launch_preprocess)
         hipExtLaunchKernelGGL(k_upsweep, dim3(nb), dim3(kThreads), 0, s, pass == 0 ? start : nullptr, nullptr, 0, kin,
                               (uint32_t)n, dev_count, shift, sc.hist, nb);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, sc.row_total);
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n, dev_count,
+                           sc.row_total);
         hipExtLaunchKernelGGL(k_downsweep, dim3(nb), dim3(kThreads), 0, s, nullptr, pass == 3 ? stop : nullptr, 0, kin,
                               vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         std::swap(kin, kout);
