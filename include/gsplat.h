@@ -107,6 +107,10 @@ int gs_ply_load(const char *path, int n, float *means4, float *colours4, float *
  * opacity, log scale, zero normals / SH).  means3, rots4, scales3, opac, colours3 as given. */
 int gs_ply_write(const char *path, int n, const float *means3, const float *rots4,
                  const float *scales3, const float *opacities, const float *colours3);
+/* saveImage (src/Splats.cpp:516-540): RGBA8 PNG of a host image (W*H*4 bytes, row y = GL
+ * row y).  flip_y = 0 writes row 0 first, as saveImage does (GL bottom row at the top of
+ * the file); 1 writes the screen orientation. */
+int gs_save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y);
 /* same activations as the loader, from raw (pre-activation) SoA records:
  * f_dc3, opacity logit, log-scale3, raw quaternion4 -> colours4, opacity, scales3, rots4 */
 int gs_activate(int n, const float *f_dc3, const float *opacity_logit, const float *log_scale3,

@@ -159,6 +159,11 @@ class Splats {
         return img;
     }
     void *texture() const { return texture_; }  // device RGBA8
+    // saveImage (src/Splats.cpp:516-540) of the current texture
+    int saveImage(const std::string &filename, bool flipY = false) const {
+        const std::vector<uint8_t> img = display();
+        return report(gs_save_png(filename.c_str(), width_, height_, img.data(), flipY ? 1 : 0));
+    }
     void setFlags(uint32_t f) { flags_ = f; }
 
     int numSplats{};

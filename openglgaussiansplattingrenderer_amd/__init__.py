@@ -11,12 +11,12 @@ from ._native import (GS_FLAG_CLEAN, GS_FLAG_DRAW_STATS, GS_FLAG_FAST_EXP, GS_FL
                       LIB_PATH, lib)
 from .splats import (Camera, Context, DeviceBuffer, GPURadixSort, PadBuffer, Splats, activate,
                      covariance3d, createAndLinkSortAndHistogramShaders, createRandomNumbersFloat, load_ply,
-                     main_camera, make_uniforms, save_ply, sort_pairs)
+                     main_camera, make_uniforms, save_ply, save_png, sort_pairs)
 
 __all__ = [
     "Camera", "Context", "DeviceBuffer", "GPURadixSort", "PadBuffer", "Splats", "activate", "covariance3d",
     "createAndLinkSortAndHistogramShaders", "createRandomNumbersFloat", "load_ply", "main_camera",
-    "make_uniforms", "save_ply", "sort_pairs", "lib", "LIB_PATH", "GsError",
+    "make_uniforms", "save_ply", "save_png", "sort_pairs", "lib", "LIB_PATH", "GsError",
     "GS_FLAG_CLEAN", "GS_FLAG_DRAW_STATS", "GS_FLAG_FAST_EXP", "GS_FLAG_TIMING", "GS_FLAG_NO_CULL",
     "GS_READ_KEYS", "GS_READ_VALS", "GS_READ_BINS", "GS_READ_MEANS2D", "GS_READ_CONICS", "GS_READ_CULLBOX",
     "GS_KERNEL_DRAW", "GS_KERNEL_SORT", "GS_TIMING_FRAME", "GS_TIMING_DRAW", "GS_TIMING_STAGES",

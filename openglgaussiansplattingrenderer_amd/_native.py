@@ -115,6 +115,7 @@ SIGNATURES = {
     "gs_ply_count": (_i, [ctypes.c_char_p, ctypes.POINTER(_i)]),
     "gs_ply_load": (_i, [ctypes.c_char_p, _i, _vp, _vp, _vp, _vp, _vp]),
     "gs_ply_write": (_i, [ctypes.c_char_p, _i, _vp, _vp, _vp, _vp, _vp]),
+    "gs_save_png": (_i, [ctypes.c_char_p, _i, _i, _vp, _i]),
     "gs_activate": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gs_covariance3d": (_i, [_i, _vp, _vp, _vp]),
     "gs_camera_update": (_i, [ctypes.POINTER(gs_camera), _vp, _vp, _fp, _fp, _fp, _fp]),

@@ -427,6 +427,9 @@ int gs_camera_uniforms(const gs_camera *cam, gs_uniforms *out) {
     if (!cam || !out || cam->height == 0) return set_error(nullptr, GS_ERR_INVALID, "bad camera");
     return gs::camera_uniforms(cam, out);
 }
+int gs_save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y) {
+    return gs::save_png(path, width, height, rgba8, flip_y);
+}
 int gs_pad_buffer(int size, int unit_width) {
     // src/sort.cpp:127-137
     if (unit_width <= 0) return 0;

@@ -7,6 +7,7 @@
 // -ffp-contract=off, so they reproduce what the reference computes on the host.
 #include "gs_internal.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -274,6 +275,81 @@ int camera_uniforms(const gs_camera *cam, gs_uniforms *u) {
     u->tan_fov_x = ty;  // main.cpp:63: camera.getTanFovy() passed as tan_fov_x (Q2)
     u->tan_fov_y = tx;  //              camera.getTanFovx() passed as tan_fov_y
     return GS_OK;
+}
+
+// ------------------------------------------------------------------ image dump
+// saveImage (src/Splats.cpp:516-540) writes an RGBA PNG whose row h is pixel row y = h of
+// the render, i.e. row 0 = the GL bottom row; flip_y = 1 writes the screen orientation
+// instead.  Self-contained writer: zlib stream of stored (uncompressed) deflate blocks.
+namespace {
+uint32_t crc32_png(const uint8_t *p, size_t n, uint32_t c = 0xffffffffu) {
+    static uint32_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t v = i;
+            for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xedb88320u ^ (v >> 1) : v >> 1;
+            table[i] = v;
+        }
+        init = true;
+    }
+    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xff] ^ (c >> 8);
+    return c;
+}
+void put_be32(std::vector<uint8_t> &v, uint32_t x) {
+    for (int s = 24; s >= 0; s -= 8) v.push_back((uint8_t)(x >> s));
+}
+void png_chunk(std::vector<uint8_t> &out, const char *type, const std::vector<uint8_t> &data) {
+    put_be32(out, (uint32_t)data.size());
+    const size_t at = out.size();
+    out.insert(out.end(), type, type + 4);
+    out.insert(out.end(), data.begin(), data.end());
+    put_be32(out, crc32_png(out.data() + at, data.size() + 4) ^ 0xffffffffu);
+}
+}  // namespace
+
+int save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y) {
+    if (!path || !rgba8 || width <= 0 || height <= 0) return set_error(nullptr, GS_ERR_INVALID, "save_png: bad argument");
+    const size_t row = (size_t)width * 4;
+    std::vector<uint8_t> raw;  // filter byte 0 + row
+    raw.reserve((row + 1) * height);
+    for (int h = 0; h < height; ++h) {
+        const int y = flip_y ? height - 1 - h : h;
+        raw.push_back(0);
+        raw.insert(raw.end(), rgba8 + (size_t)y * row, rgba8 + (size_t)(y + 1) * row);
+    }
+    std::vector<uint8_t> z = {0x78, 0x01};  // zlib header, no compression
+    uint32_t a = 1, b = 0;                   // adler32
+    for (uint8_t c : raw) {
+        a = (a + c) % 65521u;
+        b = (b + a) % 65521u;
+    }
+    for (size_t off = 0; off < raw.size() || off == 0;) {
+        const size_t len = std::min<size_t>(65535, raw.size() - off);
+        const bool last = off + len >= raw.size();
+        z.push_back(last ? 1 : 0);
+        z.push_back((uint8_t)(len & 0xff));
+        z.push_back((uint8_t)(len >> 8));
+        z.push_back((uint8_t)(~len & 0xff));
+        z.push_back((uint8_t)((~len >> 8) & 0xff));
+        z.insert(z.end(), raw.begin() + off, raw.begin() + off + len);
+        off += len;
+        if (last) break;
+    }
+    put_be32(z, (b << 16) | a);
+    std::vector<uint8_t> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    std::vector<uint8_t> ihdr;
+    put_be32(ihdr, (uint32_t)width);
+    put_be32(ihdr, (uint32_t)height);
+    ihdr.insert(ihdr.end(), {8, 6, 0, 0, 0});  // 8-bit RGBA, deflate, adaptive filter, no interlace
+    png_chunk(out, "IHDR", ihdr);
+    png_chunk(out, "IDAT", z);
+    png_chunk(out, "IEND", {});
+    FILE *f = std::fopen(path, "wb");
+    if (!f) return set_error(nullptr, GS_ERR_IO, std::string("save_png: cannot open ") + path);
+    const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok ? GS_OK : set_error(nullptr, GS_ERR_IO, std::string("save_png: write failed: ") + path);
 }
 
 }  // namespace gs

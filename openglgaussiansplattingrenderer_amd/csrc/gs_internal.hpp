@@ -25,6 +25,7 @@ int covariance3d(int n, const float *scales3, const float *rots4, float *cov6);
 int camera_update(const gs_camera *cam, float view16[16], float proj16[16], float *focal_x, float *focal_y,
                   float *tan_fovx_getter, float *tan_fovy_getter);
 int camera_uniforms(const gs_camera *cam, gs_uniforms *u);
+int save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y);
 
 // ---------------------------------------------------------------- device side
 constexpr int kTiles = 16;  // the reference's fixed 16x16 coarse grid (preprocess.glsl:143-153)

@@ -15,6 +15,7 @@ owned by a ``Context`` (one per GPU) and every stage runs as HIP kernels through
 from __future__ import annotations
 
 import ctypes
+import os
 import sys
 
 import numpy as np
@@ -297,6 +298,13 @@ def make_uniforms(view, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, v
 
 
 # ------------------------------------------------------------- loader helpers
+def save_png(filename: str, rgba8: np.ndarray, flip_y: bool = False):
+    """RGBA8 image (H, W, 4), row 0 = GL row 0, to PNG (gs_save_png)."""
+    img = np.ascontiguousarray(rgba8, np.uint8)
+    H, W = img.shape[0], img.shape[1]
+    check(lib().gs_save_png(os.fsencode(filename), int(W), int(H), ptr(img), int(flip_y)))
+
+
 def load_ply(filePath: str):
     """src/Splats.cpp:174-344 through the library's C++ loader.
     Returns means3D (N,4), colours (N,4), opacities (N,), scales (N,3), rotations (N,4)."""
@@ -469,6 +477,11 @@ class Splats:
         # no stats pointer: the frame is enqueued without a host round trip (gs_render)
         check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, self._texture.ptr, 1, None),
               self.ctx.handle)
+
+    def saveImage(self, filename: str, flip_y: bool = False):
+        """saveImage (src/Splats.cpp:516-540) of the current texture: RGBA PNG, row 0 = GL row 0
+        (flip_y=True: screen orientation)."""
+        save_png(filename, self.texture(), flip_y)
 
     def texture(self) -> np.ndarray:
         """RGBA8 image (H, W, 4); row 0 = GL row 0 (bottom of the screen)."""

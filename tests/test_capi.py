@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -63,3 +64,41 @@ def test_oracle_is_not_imported_by_product():
                 txt = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"#\s*include\s*[<\"].*gs_oracle|^\s*(from|import)\s+oracle|libgsoracle", txt,
                                      re.M), f
+
+
+def _read_png(path):
+    """minimal PNG reader (8-bit RGBA, filter 0 rows) for the writer's output"""
+    import struct
+    import zlib
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat = 8, b""
+    W = H = 0
+    while pos < len(data):
+        (n,) = struct.unpack(">I", data[pos:pos + 4])
+        typ, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        crc = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])[0]
+        assert zlib.crc32(typ + body) == crc, typ
+        if typ == b"IHDR":
+            W, H = struct.unpack(">II", body[:8])
+            assert body[8:13] == bytes([8, 6, 0, 0, 0])
+        elif typ == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = zlib.decompress(idat)
+    rows = np.frombuffer(raw, np.uint8).reshape(H, 1 + 4 * W)
+    assert np.all(rows[:, 0] == 0)
+    return rows[:, 1:].reshape(H, W, 4)
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_save_png_roundtrip(tmp_path, flip):
+    """gs_save_png (saveImage, src/Splats.cpp:516-540): row 0 first unless flipped; > 64 KiB
+    of rows spans several stored deflate blocks"""
+    import openglgaussiansplattingrenderer_amd as g
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (130, 170, 4), dtype=np.uint8)
+    p = str(tmp_path / "x.png")
+    g.save_png(p, img, flip)
+    back = _read_png(p)
+    assert np.array_equal(back, img[::-1] if flip else img)
