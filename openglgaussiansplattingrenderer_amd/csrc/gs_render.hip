@@ -549,14 +549,15 @@ __device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_bal
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <bool FAST_EXP, bool STATS>
-__global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
                                              const float4 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
                                              uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
     __shared__ float4 s_col[256];    // pixel state, pixel id = 4*lane + slot
     __shared__ uint32_t s_done[64];  // per lane: one done byte per slot
-    __shared__ uint2 s_ev[256];      // one survivor's blend events: {pixel id, power bits}
+    __shared__ float s_epow[256];    // one survivor's blend events: power ...
+    __shared__ uint8_t s_epix[256];  // ... and pixel id (split: 5.5 KB of LDS per wave -> 7 waves/SIMD)
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
@@ -701,17 +702,32 @@ __global__ __launch_bounds__(64) void k_draw(DrawParams P, const uint32_t *__res
             auto below = [&](uint64_t m, uint32_t base0) {
                 return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
             };
-            if (n00) s_ev[below(b0, 0)] = make_uint2(4 * lane + 0, __float_as_uint(p00));
-            if (n10) s_ev[below(b1, e0)] = make_uint2(4 * lane + 1, __float_as_uint(p10));
-            if (n01) s_ev[below(b2, e0 + e1)] = make_uint2(4 * lane + 2, __float_as_uint(p01));
-            if (n11) s_ev[below(b3, e0 + e1 + e2)] = make_uint2(4 * lane + 3, __float_as_uint(p11));
+            if (n00) {
+                const uint32_t e = below(b0, 0);
+                s_epow[e] = p00;
+                s_epix[e] = (uint8_t)(4 * lane + 0);
+            }
+            if (n10) {
+                const uint32_t e = below(b1, e0);
+                s_epow[e] = p10;
+                s_epix[e] = (uint8_t)(4 * lane + 1);
+            }
+            if (n01) {
+                const uint32_t e = below(b2, e0 + e1);
+                s_epow[e] = p01;
+                s_epix[e] = (uint8_t)(4 * lane + 2);
+            }
+            if (n11) {
+                const uint32_t e = below(b3, e0 + e1 + e2);
+                s_epow[e] = p11;
+                s_epix[e] = (uint8_t)(4 * lane + 3);
+            }
             wave_lds_sync();
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
             for (uint32_t e = lane; e < nev; e += 64) {
-                const uint2 ev = s_ev[e];
-                const uint32_t pix = ev.x;
-                const float power = __uint_as_float(ev.y);
+                const uint32_t pix = s_epix[e];
+                const float power = s_epow[e];
                 const float ex = FAST_EXP ? __expf(power) : exp_defined(power);
                 const float alpha = fminf(0.99f, ex * o);
                 if (alpha < 1.0f / 255.0f) continue;

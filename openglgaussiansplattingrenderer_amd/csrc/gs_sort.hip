@@ -4,7 +4,7 @@
 // computePrefixSum.glsl, scan.glsl (8 passes x 4-bit digits, 512 serial threads with
 // indirect key gathers).  Here: 4 passes x 8-bit digits, reduce-then-scan per pass with no
 // inter-workgroup communication inside a launch:
-//   k_upsweep    per 4096-key tile, 256-bin digit histogram -> hist[digit][tile]
+//   k_upsweep    per 4096-key tile (8192 in pass 0), 256-bin digit histogram -> hist[digit][tile]
 //   k_scan_rows  one workgroup per digit: exclusive scan of hist[digit][*], row totals
 //   k_downsweep  wave64 ballot-match ranking (stable), LDS reorder, coalesced scatter
 // Stability: inside a tile, wave w owns elements [w*1024, (w+1)*1024) in order and ranks them
@@ -20,12 +20,12 @@ namespace gs {
 
 namespace {
 
-constexpr int kThreads = 256;                 // 4 waves
-constexpr int kWaves = kThreads / 64;
 constexpr int kItems = 16;                    // keys per lane
-constexpr int kWaveTile = 64 * kItems;        // 1024
-constexpr int kTile = kThreads * kItems;      // 4096
+constexpr int kWaveTile = 64 * kItems;        // 1024 keys per wave
+constexpr int kWaveSmall = 4, kWaveBig = 8;   // waves per workgroup: passes 1-3 / pass 0
+constexpr int kTileSmall = kWaveSmall * kWaveTile;  // 4096
 constexpr int kRadix = 256;
+constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
@@ -60,7 +60,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// exclusive scan over the 256 threads of a block (one value each)
+// exclusive scan over the W*64 threads of a block (one value each)
+template <int W>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave) {
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t inc = wave_incl_scan(v);
@@ -68,12 +69,10 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave
     __syncthreads();
     uint32_t off = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) off += (w < wid) ? s_wave[w] : 0u;
+    for (int w = 0; w < W; ++w) off += (w < wid) ? s_wave[w] : 0u;
     __syncthreads();
     return off + inc - v;
 }
-
-constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
 // element count: n, or min(n, cnt[0] + cnt[1]) when the count lives on the device (a frame
 // enqueued without a host round trip; the grid is sized for n, the capacity)
@@ -81,9 +80,13 @@ __device__ __forceinline__ uint32_t elem_count(uint32_t n, const uint32_t *cnt) 
     return cnt ? min(n, cnt[0] + cnt[1]) : n;
 }
 
-__global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
-                                                      const uint32_t *__restrict__ cnt, int shift,
-                                                      uint32_t *__restrict__ hist, uint32_t nb) {
+// W waves per workgroup, tile = W * 1024 keys (the pass-0 sort uses W = 8: its random low
+// digits leave short runs per tile, so a larger tile doubles the scatter's write runs)
+template <int W>
+__global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
+                                                    const uint32_t *__restrict__ cnt, int shift,
+                                                    uint32_t *__restrict__ hist, uint32_t nb) {
+    constexpr int kThreads = W * 64, kTile = kThreads * kItems;
     const uint32_t n = elem_count(n_max, cnt);
     if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count (never scanned)
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
@@ -113,6 +116,7 @@ __global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict
     }
     __syncthreads();
     const int d = threadIdx.x;
+    if (d >= kRadix) return;
     const uint4 c0 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep]);
     const uint4 c1 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep + 4]);
     hist[(size_t)d * nb + blockIdx.x] = (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
@@ -121,11 +125,11 @@ __global__ __launch_bounds__(kThreads) void k_upsweep(const uint32_t *__restrict
 // one block per digit: exclusive scan of that digit's per-tile counts (the tiles holding
 // elements; rows are nb long), row total
 __global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
-                                                    const uint32_t *__restrict__ cnt,
+                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
                                                     uint32_t *__restrict__ row_total) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
-    const uint32_t nb = (elem_count(n_max, cnt) + kTile - 1) / kTile;
+    const uint32_t nb = (elem_count(n_max, cnt) + tile - 1) / tile;
     uint32_t *row = hist + (size_t)blockIdx.x * nb_stride;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry = 0;
@@ -149,11 +153,13 @@ __global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist,
     if (threadIdx.x == 0) row_total[blockIdx.x] = s_carry;
 }
 
-__global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                        uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                        uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
-                                                        const uint32_t *__restrict__ hist, uint32_t nb,
-                                                        const uint32_t *__restrict__ row_total) {
+template <int W>
+__global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                      uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                      uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
+                                                      const uint32_t *__restrict__ hist, uint32_t nb,
+                                                      const uint32_t *__restrict__ row_total) {
+    constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
     const uint32_t n = elem_count(n_max, cnt);
     if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count
     __shared__ uint32_t s_cnt[kWaves][kRadix];  // running per-wave counts -> per-wave exclusive offsets
@@ -213,18 +219,23 @@ __global__ __launch_bounds__(kThreads) void k_downsweep(const uint32_t *__restri
         rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
     __syncthreads();
     {
-        const int d = threadIdx.x;  // one thread per digit
-        uint32_t c[kWaves], tot = 0;
+        const int d = threadIdx.x;  // one thread per digit (threads >= 256 contribute zeros)
+        const bool dig = d < kRadix;
+        uint32_t tot = 0;
+        if (dig) {
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) {
-            c[w] = s_cnt[w][d];
-            s_cnt[w][d] = tot;
-            tot += c[w];
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t c = s_cnt[w][d];
+                s_cnt[w][d] = tot;
+                tot += c;
+            }
         }
-        const uint32_t start = block_excl_scan(tot, s_wave);
-        const uint32_t gdig = block_excl_scan(row_total[d], s_wave);  // digit base over the whole array
-        s_start[d] = start;
-        s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + blockIdx.x]) - (int32_t)start;
+        const uint32_t start = block_excl_scan<W>(tot, s_wave);
+        const uint32_t gdig = block_excl_scan<W>(dig ? row_total[d] : 0u, s_wave);  // digit base, whole array
+        if (dig) {
+            s_start[d] = start;
+            s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + blockIdx.x]) - (int32_t)start;
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -257,7 +268,7 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 }  // namespace
 
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s) {
-    const size_t nb = (size_t)((n + kTile - 1) / kTile);
+    const size_t nb = (size_t)((n + kTileSmall - 1) / kTileSmall);  // the most tiles of any pass
     const bool grow_alt = (size_t)n > sc.alt_cap, grow_hist = nb * kRadix > sc.hist_cap;
     if ((grow_alt && sc.keys_alt) || (grow_hist && sc.hist)) (void)hipStreamSynchronize(s);  // in-flight users
     if (grow_alt) {
@@ -310,17 +321,28 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     }
     int rc = sort_ensure(sc, n, err, s);
     if (rc) return rc;
-    const uint32_t nb = (uint32_t)((n + kTile - 1) / kTile);
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
+        const bool big = pass == 0;
+        const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
+        const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
-        hipExtLaunchKernelGGL(k_upsweep, dim3(nb), dim3(kThreads), 0, s, pass == 0 ? start : nullptr, nullptr, 0, kin,
-                              (uint32_t)n, dev_count, shift, sc.hist, nb);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n, dev_count,
+        hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
+        if (big)
+            hipExtLaunchKernelGGL(k_upsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin,
+                                  (uint32_t)n, dev_count, shift, sc.hist, nb);
+        else
+            hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
+                                  (uint32_t)n, dev_count, shift, sc.hist, nb);
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n, dev_count, tile,
                            sc.row_total);
-        hipExtLaunchKernelGGL(k_downsweep, dim3(nb), dim3(kThreads), 0, s, nullptr, pass == 3 ? stop : nullptr, 0, kin,
-                              vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+        if (big)
+            hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
+                                  kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+        else
+            hipExtLaunchKernelGGL(k_downsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin,
+                                  vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
