@@ -508,28 +508,26 @@ __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
 // <= ~6 eps * cond; conics with cond >= 1e4 are never dropped here).
 __device__ __forceinline__ bool ellipse_misses_rect(float mx, float my, float a, float b, float c, float thr,
                                                     float x0, float x1, float y0, float y1) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
     const float lim = -2.0f * thr;  // pixels with q <= lim may blend
     if (!(lim > 0.0f)) return thr > 0.0f;  // thr > 0: no power <= 0 reaches it; NaN / 0: keep
     const float det = a * c - b * b, tr = a + c;
     if (!(a > 0.0f && c > 0.0f && det > 0.0f && tr * tr < 1.0e4f * det)) return false;
-    const float X0 = x0 - mx, X1 = x1 - mx, Y0 = y0 - my, Y1 = y1 - my;
-    if (X0 <= 0.0f && X1 >= 0.0f && Y0 <= 0.0f && Y1 >= 0.0f) return false;  // centre inside
+    const f2 X = f2{x0, x1} - f2{mx, mx}, Y = f2{y0, y1} - f2{my, my};
+    if (X.x <= 0.0f && X.y >= 0.0f && Y.x <= 0.0f && Y.y >= 0.0f) return false;  // centre inside
     // edge minimisers via v_rcp (1 ulp): a minimiser off by delta raises q by O(delta^2),
-    // orders of magnitude inside the margins below
+    // orders of magnitude inside the margins below; both edges of a pair in packed fp32
     const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
-    float qmin = 3.0e38f;
+    const f2 A = f2{a, a}, B = f2{b, b}, C = f2{c, c}, two = f2{2.0f, 2.0f};
     // edges x = X0, X1: dy* = -b dx / c clamped to [Y0, Y1]
-    for (int e = 0; e < 2; ++e) {
-        const float dx = e ? X1 : X0;
-        const float dy = fminf(fmaxf(-b * dx * rc, Y0), Y1);
-        qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
-    }
+    f2 dy = -(B * X) * f2{rc, rc};
+    dy = __builtin_elementwise_min(__builtin_elementwise_max(dy, f2{Y.x, Y.x}), f2{Y.y, Y.y});
+    const f2 qx = A * X * X + two * B * X * dy + C * dy * dy;
     // edges y = Y0, Y1: dx* = -b dy / a clamped to [X0, X1]
-    for (int e = 0; e < 2; ++e) {
-        const float dy = e ? Y1 : Y0;
-        const float dx = fminf(fmaxf(-b * dy * ra, X0), X1);
-        qmin = fminf(qmin, a * dx * dx + 2.0f * b * dx * dy + c * dy * dy);
-    }
+    f2 dx = -(B * Y) * f2{ra, ra};
+    dx = __builtin_elementwise_min(__builtin_elementwise_max(dx, f2{X.x, X.x}), f2{X.y, X.y});
+    const f2 qy = A * dx * dx + two * B * dx * Y + C * Y * Y;
+    const float qmin = fminf(fminf(qx.x, qx.y), fminf(qy.x, qy.y));
     return qmin > lim * 1.002f + 1.0e-3f;
 }
 
@@ -634,10 +632,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
     // whether an entry is in the list follows from its position (chunk base + lane < end).
-    auto load_idx = [&](int base, uint32_t &v) { v = vals[min(base + lane, jmax)]; };
+    // gathers address through 32-bit byte offsets (global_load saddr form; splat ids < 2^27)
+    auto at = [](const auto *base, uint32_t byte_off) {
+        return reinterpret_cast<decltype(base)>(reinterpret_cast<const char *>(base) + byte_off);
+    };
+    auto load_idx = [&](int base, uint32_t &v) { v = *at(vals, (uint32_t)min(base + lane, jmax) << 2); };
     auto gather_box = [&](uint32_t v, uint32_t &vb, float4 &bx) {
         vb = v;
-        bx = cullbox[v];
+        bx = *at(cullbox, v << 4);
     };
     auto test_and_gather = [&](int cbase, uint32_t v, const float4 &bx, uint64_t &keep, SplatDraw &d,
                                float4 &c) {
@@ -648,8 +650,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
         // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
         const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
         const uint32_t idx = in ? v : first;
-        d = sd[idx];
-        c = colour[idx];
+        d = *at(sd, idx << 5);
+        c = *at(colour, idx << 4);
     };
     auto blend = [&](uint64_t keep, const SplatDraw &d, const float4 &c) {
         // exact cull of the survivors (uniform keep mask)
