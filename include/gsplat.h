@@ -129,6 +129,14 @@ int gs_camera_uniforms(const gs_camera *cam, gs_uniforms *out);
 int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6,
                     const float *opacity, const float *colours4, gs_scene **out);
 void gs_scene_destroy(gs_scene *scene);
+/* SURVEY f1 -- Splats(path) with the load-time work on the GPU: the ply body streams to the
+ * device and one kernel applies the activations of src/Splats.cpp:289-331 and the covariance
+ * of :414-479 with the same float operations (glibc's expf restated), so the scene equals
+ * gs_ply_load + gs_covariance3d + gs_scene_create bit for bit.  Host arrays are not produced
+ * (gs_scene_download fetches them).  Same errors and messages as gs_ply_load. */
+int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out);
+/* the scene's arrays in gs_scene_create's host layout (means4 w = 1); any may be NULL */
+int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *opacity, float *colours4);
 int gs_scene_count(const gs_scene *scene);
 
 /* ---------------------------------------------------------------- frame

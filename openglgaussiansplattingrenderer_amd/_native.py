@@ -121,6 +121,8 @@ SIGNATURES = {
     "gs_camera_update": (_i, [ctypes.POINTER(gs_camera), _vp, _vp, _fp, _fp, _fp, _fp]),
     "gs_camera_uniforms": (_i, [ctypes.POINTER(gs_camera), ctypes.POINTER(gs_uniforms)]),
     "gs_scene_create": (_i, [_vp, _i, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+    "gs_scene_load_ply": (_i, [_vp, ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    "gs_scene_download": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "gs_scene_destroy": (None, [_vp]),
     "gs_scene_count": (_i, [_vp]),
     "gs_render": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, _vp, _i, ctypes.POINTER(gs_frame_stats)]),

@@ -470,6 +470,92 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
     return GS_OK;
 }
 
+// the load path on the GPU.  The ply body streams through two pinned chunk
+// buffers (fread -> async H2D -> k_ply_activate), so reading, copying and the activations of
+// consecutive chunks overlap; the scene equals gs_ply_load + gs_covariance3d +
+// gs_scene_create bit for bit (gs_load.hip).  No host-side arrays are produced.
+int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out) {
+    if (!ctx || !path || !out) return set_error(ctx, GS_ERR_INVALID, "gs_scene_load_ply: null argument");
+    *out = nullptr;
+    if (int rc = use_device(ctx)) return rc;
+    int n = 0;
+    std::FILE *f = nullptr;
+    if (int rc = gs::ply_open_body(path, &n, &f)) return set_error(ctx, rc, gs_last_error(nullptr));
+    const size_t nn = (size_t)n, rec = gs::kPlyFloats * sizeof(float);
+    gs_scene *s = new gs_scene();
+    s->ctx = ctx;
+    s->n = n;
+    constexpr size_t kChunk = 1 << 18;  // splats per chunk (65 MB of records)
+    float *h_buf[2] = {nullptr, nullptr}, *d_buf[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    auto cleanup = [&](int rc, const std::string &msg) {
+        (void)hipStreamSynchronize(ctx->stream);
+        for (int k = 0; k < 2; ++k) {
+            if (h_buf[k]) (void)hipHostFree(h_buf[k]);
+            if (d_buf[k]) (void)hipFree(d_buf[k]);
+            if (done[k]) (void)hipEventDestroy(done[k]);
+        }
+        std::fclose(f);
+        if (rc) {
+            gs_scene_destroy(s);
+            return set_error(ctx, rc, msg);
+        }
+        return GS_OK;
+    };
+    if (hipMalloc(&s->soa, 10 * std::max<size_t>(nn, 1) * 4) != hipSuccess ||
+        hipMalloc(&s->colour, std::max<size_t>(nn, 1) * sizeof(float4)) != hipSuccess)
+        return cleanup(GS_ERR_NOMEM, "gs_scene_load_ply: out of device memory");
+    const size_t chunk = std::min(kChunk, std::max<size_t>(nn, 1));
+    for (int k = 0; k < 2; ++k)
+        if (hipHostMalloc(&h_buf[k], chunk * rec, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(&d_buf[k], chunk * rec) != hipSuccess || hipEventCreate(&done[k]) != hipSuccess)
+            return cleanup(GS_ERR_NOMEM, "gs_scene_load_ply: staging allocation failed");
+    for (size_t base = 0, it = 0; base < nn; base += chunk, ++it) {
+        const int k = (int)(it & 1);
+        const size_t cnt = std::min(chunk, nn - base);
+        if (it >= 2 && hipEventSynchronize(done[k]) != hipSuccess)  // copy out of h_buf[k] finished
+            return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipEventSynchronize failed");
+        if (std::fread(h_buf[k], rec, cnt, f) != cnt)  // src/Splats.cpp:333-340
+            return cleanup(GS_ERR_IO, "Error: failed to read all splats from file");
+        if (hipMemcpyAsync(d_buf[k], h_buf[k], cnt * rec, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipMemcpyAsync failed");
+        gs::launch_ply_activate(ctx->stream, d_buf[k], (int)cnt, (int)base, n, s->soa, s->colour);
+        if (hipEventRecord(done[k], ctx->stream) != hipSuccess)
+            return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipEventRecord failed");
+    }
+    if (std::fgetc(f) != EOF) return cleanup(GS_ERR_IO, "Error: failed to read all splats from file");
+    if (hipGetLastError() != hipSuccess) return cleanup(GS_ERR_HIP, "gs_scene_load_ply: kernel launch failed");
+    if (int rc = cleanup(GS_OK, "")) return rc;
+    ctx->scenes.push_back(s);
+    *out = s;
+    return GS_OK;
+}
+
+// the scene's arrays in the host layout of gs_scene_create (means4 w = 1); any may be NULL
+int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *opacity, float *colours4) {
+    if (!scene || !scene->ctx) return set_error(nullptr, GS_ERR_INVALID, "gs_scene_download: bad scene");
+    gs_ctx *ctx = scene->ctx;
+    if (int rc = use_device(ctx)) return rc;
+    const size_t nn = (size_t)scene->n;
+    std::vector<float> soa(10 * nn);
+    if (nn) GS_HIP(ctx, hipMemcpyAsync(soa.data(), scene->soa, soa.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (nn && colours4)
+        GS_HIP(ctx, hipMemcpyAsync(colours4, scene->colour, nn * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < nn; ++i) {
+        if (means4) {
+            means4[4 * i + 0] = soa[i];
+            means4[4 * i + 1] = soa[nn + i];
+            means4[4 * i + 2] = soa[2 * nn + i];
+            means4[4 * i + 3] = 1.f;
+        }
+        if (cov6)
+            for (int c = 0; c < 6; ++c) cov6[6 * i + c] = soa[(3 + c) * nn + i];
+        if (opacity) opacity[i] = soa[9 * nn + i];
+    }
+    return GS_OK;
+}
+
 void gs_scene_destroy(gs_scene *scene) {
     if (!scene) return;
     if (gs_ctx *ctx = scene->ctx) {

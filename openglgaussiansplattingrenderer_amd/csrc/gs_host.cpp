@@ -109,6 +109,23 @@ int ply_count(const char *path, int *n) {
     return GS_OK;
 }
 
+// the ply's vertex count and a FILE positioned at its body (src/Splats.cpp:252-267)
+int ply_open_body(const char *path, int *n, std::FILE **out) {
+    if (int rc = ply_count(path, n)) return rc;
+    std::FILE *f = std::fopen(path, "rb");
+    if (!f) return set_error(nullptr, GS_ERR_IO, std::string("Error: failed to open file ") + path);
+    std::string line;
+    for (int i = 0; i < 3; ++i) read_line(f, line);
+    while (line != "end_header") {
+        if (!read_line(f, line)) {
+            std::fclose(f);
+            return set_error(nullptr, GS_ERR_IO, "Error: no end_header in ply");
+        }
+    }
+    *out = f;
+    return GS_OK;
+}
+
 // One splat's activations (src/Splats.cpp:289-331); shared by the loader and gs_activate.
 static inline void activate_one(const float *f_dc, float opac_logit, const float *log_scale,
                                 const float *rot, float *colour4, float *opacity, float *scale3,

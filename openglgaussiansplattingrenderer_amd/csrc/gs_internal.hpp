@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <string>
 
 #include "../../include/gsplat.h"
@@ -15,6 +16,7 @@ int set_error(gs_ctx *ctx, int code, const std::string &msg);
 
 // host side (gs_host.cpp)
 int ply_count(const char *path, int *n);
+int ply_open_body(const char *path, int *n, std::FILE **out);
 int ply_load(const char *path, int n, float *means4, float *colours4, float *opacity, float *scales3,
              float *rots4);
 int ply_write(const char *path, int n, const float *means3, const float *rots4, const float *scales3,
@@ -107,6 +109,11 @@ void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint3
 // zero on entry and are left zero
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,
                  uint32_t *bins, hipEvent_t stop);
+// GPU load path (gs_load.hip): count raw 62-float ply records starting at splat `base` ->
+// the scene's SoA planes (n floats each: mx my mz cov0..5 opacity) and colours
+constexpr int kPlyFloats = 62;
+void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, int n, float *soa, float4 *colour);
+
 // GS_FLAG_DRAW_STATS buffer: 16 counters, then per block {start, end} (s_memrealtime, 100 MHz),
 // iterations, survivors
 constexpr int kDrawTraceBlocks = 65536;

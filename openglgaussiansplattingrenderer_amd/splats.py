@@ -362,10 +362,14 @@ class Splats:
     GS_FLAG_CLEAN, and the blend's exp (bit-exact polynomial or GS_FLAG_FAST_EXP)."""
 
     def __init__(self, filePath: str | None, width: int, height: int, *, ctx: Context | None = None,
-                 device: int = 0, flags: int = 0, arrays=None):
+                 device: int = 0, flags: int = 0, arrays=None, gpu_load: bool = False):
         self.ctx = ctx if ctx is not None else Context(device)
         self.flags = int(flags)
         print("setting up splats", file=sys.stderr)
+        if gpu_load:  # SURVEY f1: activations + covariance on the GPU (gs_scene_load_ply)
+            self._load_gpu(filePath, width, height)
+            print("finished setting up splats", file=sys.stderr)
+            return
         if arrays is None:
             self.loadSplats(filePath)
         else:
@@ -384,6 +388,28 @@ class Splats:
         m = np.ascontiguousarray(means3, np.float32).reshape(-1, 3)
         means4 = np.concatenate([m, np.ones((len(m), 1), np.float32)], axis=1)
         return cls(None, width, height, arrays=(means4, cols, op, sc, rot), **kw)
+
+    def _load_gpu(self, filePath: str, width: int, height: int):
+        h = ctypes.c_void_p()
+        check(lib().gs_scene_load_ply(self.ctx.handle, os.fsencode(filePath), ctypes.byref(h)), self.ctx.handle)
+        self._scene = h
+        self.numSplats = int(lib().gs_scene_count(h))
+        empty = np.zeros((0, 4), np.float32)
+        self.means3D = self.colours = self.rotations = empty
+        self.opacities, self.scales = np.zeros(0, np.float32), np.zeros((0, 3), np.float32)
+        self.covarianceMatrices = np.zeros(0, np.float32)
+        self.sphericalHarmonics = np.zeros(0, np.float32)
+        self.width, self.height = int(width), int(height)
+        self._texture = DeviceBuffer(self.ctx, self.width * self.height * 4)
+        self._stats = N.gs_frame_stats()
+
+    def download(self):
+        """(means4, cov6, opacity, colours4) of the device scene (gs_scene_download)"""
+        n = self.numSplats
+        m, c, o, col = (np.zeros(4 * n, np.float32), np.zeros(6 * n, np.float32), np.zeros(n, np.float32),
+                        np.zeros(4 * n, np.float32))
+        check(lib().gs_scene_download(self._scene, ptr(m), ptr(c), ptr(o), ptr(col)), self.ctx.handle)
+        return m.reshape(n, 4), c, o, col.reshape(n, 4)
 
     # src/Splats.cpp:174-344
     def loadSplats(self, filePath: str):
