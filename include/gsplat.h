@@ -38,6 +38,9 @@ extern "C" {
 #define GS_FLAG_TIMING 4u    /* record per-stage hipEvent timings into gs_frame_stats */
 #define GS_FLAG_NO_CULL 8u   /* disable the (exactness-preserving) per-block entry cull */
 #define GS_FLAG_DRAW_STATS 16u /* count blend work (see gs_draw_stats); slower, diagnostics only */
+#define GS_FLAG_SH 64u       /* SURVEY f3, beyond the reference: view-dependent colour from degree-3
+                              * spherical harmonics (scene needs gs_scene_set_sh); the reference
+                              * reads f_rest and discards it (src/Splats.cpp:300-302) */
 
 typedef struct gs_ctx gs_ctx;
 typedef struct gs_scene gs_scene;
@@ -103,6 +106,9 @@ int gs_ply_count(const char *path, int *n);
  * opacity sigmoid, scales3 exp, rots4 normalised (rot_0..rot_3).  Any output may be NULL. */
 int gs_ply_load(const char *path, int n, float *means4, float *colours4, float *opacity,
                 float *scales3, float *rots4);
+/* the raw SH fields of the ply (f_dc_0..2 and f_rest_0..44, as stored: f_rest is channel-major,
+ * 15 coefficients per channel) -- what loadSplats reads and drops (src/Splats.cpp:286-302) */
+int gs_ply_load_sh(const char *path, int n, float *f_dc3, float *f_rest45);
 /* tests/plyFileGenerator.py:155-249 save_ply byte layout (raw colours into f_dc, logit
  * opacity, log scale, zero normals / SH).  means3, rots4, scales3, opac, colours3 as given. */
 int gs_ply_write(const char *path, int n, const float *means3, const float *rots4,
@@ -137,6 +143,11 @@ void gs_scene_destroy(gs_scene *scene);
 int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out);
 /* the scene's arrays in gs_scene_create's host layout (means4 w = 1); any may be NULL */
 int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *opacity, float *colours4);
+/* attach degree-3 SH (raw f_dc3 + f_rest45 per splat, ply layout) to a scene;
+ * GS_FLAG_SH frames then colour each splat by the standard 3DGS evaluation for the direction
+ * from the camera: max(SH(dir) + 0.5, 0) * 255 (with f_rest = 0 this is the reference's
+ * colour wherever that is non-negative) */
+int gs_scene_set_sh(gs_scene *scene, const float *f_dc3, const float *f_rest45);
 int gs_scene_count(const gs_scene *scene);
 
 /* ---------------------------------------------------------------- frame

@@ -23,6 +23,7 @@ GS_FLAG_FAST_EXP = 2
 GS_FLAG_TIMING = 4
 GS_FLAG_NO_CULL = 8
 GS_FLAG_DRAW_STATS = 16
+GS_FLAG_SH = 64
 
 GS_READ_KEYS = 1
 GS_READ_VALS = 2
@@ -123,6 +124,8 @@ SIGNATURES = {
     "gs_scene_create": (_i, [_vp, _i, _vp, _vp, _vp, _vp, ctypes.POINTER(_vp)]),
     "gs_scene_load_ply": (_i, [_vp, ctypes.c_char_p, ctypes.POINTER(_vp)]),
     "gs_scene_download": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "gs_scene_set_sh": (_i, [_vp, _vp, _vp]),
+    "gs_ply_load_sh": (_i, [ctypes.c_char_p, _i, _vp, _vp]),
     "gs_scene_destroy": (None, [_vp]),
     "gs_scene_count": (_i, [_vp]),
     "gs_render": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, _vp, _i, ctypes.POINTER(gs_frame_stats)]),

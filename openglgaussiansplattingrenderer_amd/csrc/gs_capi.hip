@@ -26,6 +26,8 @@ struct gs_ctx {
     // per-splat frame buffers (sized by the largest scene rendered so far)
     int n_cap = 0;
     gs::SplatDraw *sd = nullptr;
+    float4 *col = nullptr;  // per-frame colours of GS_FLAG_SH frames
+    int col_cap = 0;
     float4 *cullbox = nullptr;
     int4 *rec = nullptr;
     uint2 *blocksum = nullptr;
@@ -84,6 +86,7 @@ struct gs_scene {
     int n = 0;
     float *soa = nullptr;       // mx | my | mz | cov0..cov5 | opacity  (10 planes of n floats)
     float4 *colour = nullptr;   // (r,g,b,1)
+    float *sh = nullptr;        // GS_FLAG_SH: 48 planes of n floats (channel c, coefficient k -> 16c + k)
 };
 
 namespace gs {
@@ -154,6 +157,7 @@ gs::FrameDev frame_dev(gs_ctx *ctx) {
     f.blocksum = ctx->blocksum;
     f.totals = ctx->totals;
     f.h_totals = ctx->h_ring_dev + 4 * ctx->cur;
+    f.col = ctx->col;
     return f;
 }
 
@@ -167,6 +171,7 @@ gs::SceneDev scene_dev(const gs_scene *s) {
     d.cov = s->soa + 3 * n;
     d.opacity = s->soa + 9 * n;
     d.colour = s->colour;
+    d.sh = s->sh;
     return d;
 }
 
@@ -341,8 +346,8 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
-    void *bufs[] = {ctx->sd, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys,
-                    ctx->vals, ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats};
+    void *bufs[] = {ctx->sd, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys, ctx->vals,
+                    ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats, ctx->col};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
@@ -430,6 +435,9 @@ int gs_camera_update(const gs_camera *cam, float view16[16], float proj16[16], f
 int gs_camera_uniforms(const gs_camera *cam, gs_uniforms *out) {
     if (!cam || !out || cam->height == 0) return set_error(nullptr, GS_ERR_INVALID, "bad camera");
     return gs::camera_uniforms(cam, out);
+}
+int gs_ply_load_sh(const char *path, int n, float *f_dc3, float *f_rest45) {
+    return gs::ply_load_sh(path, n, f_dc3, f_rest45);
 }
 int gs_save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y) {
     return gs::save_png(path, width, height, rgba8, flip_y);
@@ -590,6 +598,26 @@ int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *
     return GS_OK;
 }
 
+int gs_scene_set_sh(gs_scene *scene, const float *f_dc3, const float *f_rest45) {
+    if (!scene || !scene->ctx || (scene->n > 0 && (!f_dc3 || !f_rest45)))
+        return set_error(nullptr, GS_ERR_INVALID, "gs_scene_set_sh: bad argument");
+    gs_ctx *ctx = scene->ctx;
+    if (int rc = use_device(ctx)) return rc;
+    if (int rc = gs_sync(ctx)) return rc;  // frames in flight may read the old planes
+    const size_t n = (size_t)scene->n;
+    std::vector<float> planes(48 * std::max<size_t>(n, 1));
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < 3; ++c) {
+            planes[(size_t)(16 * c) * n + i] = f_dc3[3 * i + c];
+            for (int k = 1; k < 16; ++k) planes[(size_t)(16 * c + k) * n + i] = f_rest45[45 * i + 15 * c + (k - 1)];
+        }
+    if (!scene->sh && hipMalloc(&scene->sh, planes.size() * 4) != hipSuccess)
+        return set_error(ctx, GS_ERR_NOMEM, "gs_scene_set_sh: out of device memory");
+    GS_HIP(ctx, hipMemcpyAsync(scene->sh, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return GS_OK;
+}
+
 void gs_scene_destroy(gs_scene *scene) {
     if (!scene) return;
     if (gs_ctx *ctx = scene->ctx) {
@@ -599,6 +627,7 @@ void gs_scene_destroy(gs_scene *scene) {
     }
     if (scene->soa) (void)hipFree(scene->soa);
     if (scene->colour) (void)hipFree(scene->colour);
+    if (scene->sh) (void)hipFree(scene->sh);
     delete scene;
 }
 
@@ -641,10 +670,21 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 // preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->totals
 int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {
     const int n = scene->n;
+    const bool sh = (flags & GS_FLAG_SH) != 0;
+    if (sh && !scene->sh) return set_error(ctx, GS_ERR_INVALID, "GS_FLAG_SH: the scene has no SH (gs_scene_set_sh)");
     if (int rc = ensure_splats(ctx, n)) return rc;
+    if (sh && ctx->col_cap < n) {
+        if (int rc = grow(ctx, ctx->col, (size_t)n)) return rc;
+        ctx->col_cap = n;
+    }
     if (int rc = begin_frame(ctx)) return rc;
     ctx->flags = flags;
-    const gs::PreParams P = pre_params(u, flags, n);
+    gs::PreParams P = pre_params(u, flags, n);
+    P.sh = sh ? 1 : 0;
+    // camera position = -R^T t of the view matrix (column-major, view[4c + r])
+    for (int c = 0; c < 3; ++c)
+        P.campos[c] = -(u->view[4 * c + 0] * u->view[12] + u->view[4 * c + 1] * u->view[13] +
+                        u->view[4 * c + 2] * u->view[14]);
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = gs::preprocess_blocks(n);
     // k_scan_blocksums writes (V, D) to ctx->totals and to this slot's pinned host copy
@@ -721,8 +761,9 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     }
     P.coverW = coverW;
     P.coverH = coverH;
-    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx),
-                    scene->colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
+    // GS_FLAG_SH frames blend the colours their preprocess evaluated
+    const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->col : scene->colour;
+    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
                     fev(ctx, 8));
     GS_HIP(ctx, hipGetLastError());
     if (!out_on_device) {

@@ -187,6 +187,33 @@ int ply_load(const char *path, int n, float *means4, float *colours4, float *opa
     return GS_OK;
 }
 
+int ply_load_sh(const char *path, int n, float *f_dc3, float *f_rest45) {
+    int cnt_file = 0;
+    std::FILE *f = nullptr;
+    if (int rc = ply_open_body(path, &cnt_file, &f)) return rc;
+    if (cnt_file != n) {
+        std::fclose(f);
+        return set_error(nullptr, GS_ERR_INVALID, "ply_load_sh: n differs from the file's vertex count");
+    }
+    const int kRec = 62, kBlock = 1 << 16;
+    std::vector<float> buf(static_cast<size_t>(kBlock) * kRec);
+    for (int base = 0; base < n; base += kBlock) {
+        const int cnt = std::min(kBlock, n - base);
+        if (std::fread(buf.data(), sizeof(float) * kRec, cnt, f) != static_cast<size_t>(cnt)) {
+            std::fclose(f);
+            return set_error(nullptr, GS_ERR_IO, "Error: failed to read all splats from file");
+        }
+        for (int j = 0; j < cnt; ++j) {
+            const size_t i = static_cast<size_t>(base) + j;
+            const float *rec = buf.data() + static_cast<size_t>(j) * kRec;
+            if (f_dc3) std::memcpy(f_dc3 + 3 * i, rec + 6, 3 * sizeof(float));
+            if (f_rest45) std::memcpy(f_rest45 + 45 * i, rec + 9, 45 * sizeof(float));
+        }
+    }
+    std::fclose(f);
+    return GS_OK;
+}
+
 int ply_write(const char *path, int n, const float *means3, const float *rots4, const float *scales3,
               const float *opacities, const float *colours3) {
     std::FILE *f = std::fopen(path, "wb");

@@ -17,6 +17,7 @@ int set_error(gs_ctx *ctx, int code, const std::string &msg);
 // host side (gs_host.cpp)
 int ply_count(const char *path, int *n);
 int ply_open_body(const char *path, int *n, std::FILE **out);
+int ply_load_sh(const char *path, int n, float *f_dc3, float *f_rest45);
 int ply_load(const char *path, int n, float *means4, float *colours4, float *opacity, float *scales3,
              float *rots4);
 int ply_write(const char *path, int n, const float *means3, const float *rots4, const float *scales3,
@@ -41,6 +42,8 @@ struct PreParams {
     float tile_w, tile_h;  // int-derived (ref, Q4) or float (clean)
     int32_t clean;
     int32_t n;
+    int32_t sh;            // GS_FLAG_SH: colours from degree-3 SH (SceneDev::sh) -> FrameDev::col
+    float campos[3];       // camera position in world space (for the SH direction)
 };
 
 // Per-frame parameters of the blend kernel (draw.glsl:38-47)
@@ -83,6 +86,7 @@ struct SceneDev {
     const float *cov;            // 6 SoA planes of n floats: [S00 | S01 | S02 | S11 | S12 | S22]
     const float *opacity;
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
+    const float *sh;             // 48 SoA planes (channel c, coefficient k -> plane 16c + k) or null
 };
 // per-splat blend inputs, one 32-byte aligned record (the blend gathers it with the colour)
 struct alignas(32) SplatDraw {
@@ -98,6 +102,7 @@ struct FrameDev {
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
     uint32_t *totals;  // [0]=V [1]=D
     uint32_t *h_totals;  // mapped pinned host copy of (V, D) for this frame, or null
+    float4 *col;         // per-frame colours of GS_FLAG_SH frames (else null)
 };
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
 // start / stop: optional hipEvents recorded on the dispatch packets (stage timing)

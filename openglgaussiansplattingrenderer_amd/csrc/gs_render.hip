@@ -112,6 +112,32 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w
     return off + inc - v;
 }
 
+// ------------------------------------------------------------------ SH colour
+// SURVEY f3 (beyond the reference, GS_FLAG_SH): degree-3 real spherical harmonics in the
+// standard 3D Gaussian Splatting convention (coefficients SH_C0..SH_C3, the evaluation order of
+// its computeColorFromSH), for the direction from the camera to the splat; colour =
+// max(SH + 0.5, 0) * 255 so that with f_rest = 0 it is the reference's (0.5 + SH_C0 * f_dc) * 255
+// wherever that is non-negative.  The oracle (ora_sh_colours) evaluates the same op sequence.
+__device__ __forceinline__ float sh_channel(const float *sh, size_t n, size_t i, int c, float x, float y, float z) {
+    const float SH_C0 = 0.28209479177387814f, SH_C1 = 0.4886025119029199f;
+    const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
+                            0.5462742152960396f};
+    const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
+                            -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
+    const float *k = sh + (size_t)(16 * c) * n + i;  // plane 16c + j holds coefficient j of channel c
+    float r = SH_C0 * k[0];
+    r = r - SH_C1 * y * k[n] + SH_C1 * z * k[2 * n] - SH_C1 * x * k[3 * n];
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    r = r + SH_C2[0] * xy * k[4 * n] + SH_C2[1] * yz * k[5 * n] + SH_C2[2] * (2.0f * zz - xx - yy) * k[6 * n] +
+        SH_C2[3] * xz * k[7 * n] + SH_C2[4] * (xx - yy) * k[8 * n];
+    r = r + SH_C3[0] * y * (3.0f * xx - yy) * k[9 * n] + SH_C3[1] * xy * z * k[10 * n] +
+        SH_C3[2] * y * (4.0f * zz - xx - yy) * k[11 * n] + SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * k[12 * n] +
+        SH_C3[4] * x * (4.0f * zz - xx - yy) * k[13 * n] + SH_C3[5] * z * (xx - yy) * k[14 * n] +
+        SH_C3[6] * x * (xx - 3.0f * yy) * k[15 * n];
+    r = r + 0.5f;
+    return fmaxf(r, 0.0f) * 255.0f;
+}
+
 // ------------------------------------------------------------------ preprocess
 // kPer splats per lane, striped (splat = block*kSplatsPerBlock + k*256 + lane) so every load
 // stays coalesced; one (main, dup) sum per workgroup feeds the emission scan.
@@ -227,6 +253,16 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends), NaN never skips
         const float thr = -logf(255.0f * co.w) - 1.0e-3f;
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
+        if (P.sh && rc.y >= 0) {  // GS_FLAG_SH: this frame's colour of a splat that has entries
+            float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
+            const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+            dx = dx / len;
+            dy = dy / len;
+            dz = dz / len;
+            const size_t n = (size_t)P.n;
+            fr.col[i] = make_float4(sh_channel(sc.sh, n, i, 0, dx, dy, dz), sh_channel(sc.sh, n, i, 1, dx, dy, dz),
+                                    sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
+        }
         fr.cullbox[i] = box;
         fr.rec[i] = rc;
     }

@@ -298,6 +298,14 @@ def make_uniforms(view, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, v
 
 
 # ------------------------------------------------------------- loader helpers
+def load_ply_sh(path: str, n: int):
+    """raw (f_dc3 (n,3), f_rest45 (n,45)) of a ply -- the fields loadSplats drops"""
+    d = np.zeros((n, 3), np.float32)
+    r = np.zeros((n, 45), np.float32)
+    check(lib().gs_ply_load_sh(os.fsencode(path), int(n), ptr(d), ptr(r)))
+    return d, r
+
+
 def save_png(filename: str, rgba8: np.ndarray, flip_y: bool = False):
     """RGBA8 image (H, W, 4), row 0 = GL row 0, to PNG (gs_save_png)."""
     img = np.ascontiguousarray(rgba8, np.uint8)
@@ -362,12 +370,14 @@ class Splats:
     GS_FLAG_CLEAN, and the blend's exp (bit-exact polynomial or GS_FLAG_FAST_EXP)."""
 
     def __init__(self, filePath: str | None, width: int, height: int, *, ctx: Context | None = None,
-                 device: int = 0, flags: int = 0, arrays=None, gpu_load: bool = False):
+                 device: int = 0, flags: int = 0, arrays=None, gpu_load: bool = False, sh: bool = False):
         self.ctx = ctx if ctx is not None else Context(device)
         self.flags = int(flags)
         print("setting up splats", file=sys.stderr)
         if gpu_load:  # SURVEY f1: activations + covariance on the GPU (gs_scene_load_ply)
             self._load_gpu(filePath, width, height)
+            if sh:
+                self.set_sh(*load_ply_sh(filePath, self.numSplats))
             print("finished setting up splats", file=sys.stderr)
             return
         if arrays is None:
@@ -379,7 +389,17 @@ class Splats:
         self.computeCovarianceMatrices()
         self._scene = None
         self.loadToGPU(width, height)
+        if sh and filePath is not None:  # keep the f_rest the reference discards
+            self.set_sh(*load_ply_sh(filePath, self.numSplats))
         print("finished setting up splats", file=sys.stderr)
+
+    def set_sh(self, f_dc3, f_rest45):
+        """attach degree-3 SH (raw f_dc, f_rest in ply layout) for GS_FLAG_SH frames"""
+        d = np.ascontiguousarray(f_dc3, np.float32).reshape(-1, 3)
+        r = np.ascontiguousarray(f_rest45, np.float32).reshape(-1, 45)
+        assert len(d) == len(r) == self.numSplats
+        check(lib().gs_scene_set_sh(self._scene, ptr(d), ptr(r)), self.ctx.handle)
+        self.sphericalHarmonics = np.concatenate([d, r], axis=1)
 
     @classmethod
     def from_raw(cls, means3, f_dc, opacity_logit, log_scale, rot_raw, width, height, **kw) -> "Splats":

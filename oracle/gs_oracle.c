@@ -495,3 +495,51 @@ void ora_draw_rows(int W, int H, uint32_t flags, const uint32_t *bins256, const 
         }
     }
 }
+
+/* ---------------------------------------------------------------- SH colour (f3) */
+
+static float ora_sh_channel(const float *k16, float x, float y, float z)
+{
+    /* k16[0] = f_dc, k16[1..15] = f_rest of one channel; evaluation order of the standard 3DGS
+     * computeColorFromSH (the kernel's sh_channel evaluates the same sequence) */
+    const float SH_C0 = 0.28209479177387814f, SH_C1 = 0.4886025119029199f;
+    const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
+                            0.5462742152960396f};
+    const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
+                            -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
+    float r = SH_C0 * k16[0];
+    r = r - SH_C1 * y * k16[1] + SH_C1 * z * k16[2] - SH_C1 * x * k16[3];
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    r = r + SH_C2[0] * xy * k16[4] + SH_C2[1] * yz * k16[5] + SH_C2[2] * (2.0f * zz - xx - yy) * k16[6] +
+        SH_C2[3] * xz * k16[7] + SH_C2[4] * (xx - yy) * k16[8];
+    r = r + SH_C3[0] * y * (3.0f * xx - yy) * k16[9] + SH_C3[1] * xy * z * k16[10] +
+        SH_C3[2] * y * (4.0f * zz - xx - yy) * k16[11] + SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * k16[12] +
+        SH_C3[4] * x * (4.0f * zz - xx - yy) * k16[13] + SH_C3[5] * z * (xx - yy) * k16[14] +
+        SH_C3[6] * x * (xx - 3.0f * yy) * k16[15];
+    r = r + 0.5f;
+    return fmaxf(r, 0.0f) * 255.0f;
+}
+
+void ora_sh_colours(int n, const float *means4, const float *f_dc3, const float *f_rest45, const float *view16,
+                    const uint8_t *visible, float *colours4)
+{
+    float campos[3];
+    for (int c = 0; c < 3; ++c)
+        campos[c] = -(view16[4 * c + 0] * view16[12] + view16[4 * c + 1] * view16[13] + view16[4 * c + 2] * view16[14]);
+    #pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; ++i) {
+        if (!visible[i]) continue;
+        float dx = means4[4 * i] - campos[0], dy = means4[4 * i + 1] - campos[1], dz = means4[4 * i + 2] - campos[2];
+        const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+        dx = dx / len;
+        dy = dy / len;
+        dz = dz / len;
+        for (int c = 0; c < 3; ++c) {
+            float k16[16];
+            k16[0] = f_dc3[3 * (size_t)i + c];
+            for (int k = 1; k < 16; ++k) k16[k] = f_rest45[45 * (size_t)i + 15 * c + (k - 1)];
+            colours4[4 * (size_t)i + c] = ora_sh_channel(k16, dx, dy, dz);
+        }
+        colours4[4 * (size_t)i + 3] = 1.0f;
+    }
+}

@@ -97,6 +97,13 @@ void ora_draw_rows(int W, int H, uint32_t flags, const uint32_t *bins256, const 
 /* the exp used by the blend (draw.glsl:122); exported for tests */
 float ora_expf(float x);
 
+/* SURVEY f3 (beyond the reference; GS_FLAG_SH): colours4[i] = (max(SH(dir)+0.5, 0)*255, 1) with
+ * dir = normalize(mean - campos), campos = -R^T t of view16, degree-3 SH in the standard 3D
+ * Gaussian Splatting convention (f_dc3 raw, f_rest45 channel-major as in the ply).  Only
+ * splats with visible[i] != 0 are written.  Not pinned by the reference (it has no SH). */
+void ora_sh_colours(int n, const float *means4, const float *f_dc3, const float *f_rest45, const float *view16,
+                    const uint8_t *visible, float *colours4);
+
 /* OpenMP threads the oracle uses (for the cpu_baseline "cores" field) */
 int ora_num_threads(void);
 

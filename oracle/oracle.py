@@ -38,6 +38,7 @@ def lib():
             "ora_ply_count": (ctypes.c_int, [ctypes.c_char_p]),
             "ora_ply_load": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, vp, vp, vp, vp, vp]),
             "ora_cov3d": (None, [ctypes.c_int, vp, vp, vp]),
+            "ora_sh_colours": (None, [ctypes.c_int, vp, vp, vp, vp, vp, vp]),
             "ora_preprocess": (None, [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_uint32,
                                       vp, vp, vp, vp, vp, vp]),
@@ -105,6 +106,18 @@ def cov3d(scales, rots) -> np.ndarray:
     r = np.ascontiguousarray(rots, np.float32)
     out = np.zeros(6 * len(s), np.float32)
     lib().ora_cov3d(len(s), _p(s), _p(r), _p(out))
+    return out
+
+
+def sh_colours(means4, f_dc3, f_rest45, view16, visible, colours4) -> np.ndarray:
+    """SURVEY f3 colours (GS_FLAG_SH) of the visible splats; others keep colours4's values"""
+    m = np.ascontiguousarray(means4, np.float32)
+    d = np.ascontiguousarray(f_dc3, np.float32)
+    r = np.ascontiguousarray(f_rest45, np.float32)
+    v = np.ascontiguousarray(view16, np.float32)
+    vis = np.ascontiguousarray(visible, np.uint8)
+    out = np.array(colours4, np.float32, copy=True, order="C")
+    lib().ora_sh_colours(len(m), _p(m), _p(d), _p(r), _p(v), _p(vis), _p(out))
     return out
 
 

@@ -1,0 +1,106 @@
+"""SURVEY f3 (beyond the reference): view-dependent colour from degree-3 SH (GS_FLAG_SH).
+CPU: the ply's raw SH fields round-trip through gs_ply_load_sh.  GPU: frames are bit-exact
+against the oracle's SH colours rendered by the oracle; with f_rest = 0 the SH path gives the
+reference's colour (image identical to the default path)."""
+import os
+
+import numpy as np
+import pytest
+
+import openglgaussiansplattingrenderer_amd as g
+from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+
+
+def write_ply_with_sh(path, means, f_dc, f_rest, logit, log_scale, rot):
+    """ply in the tests/plyFileGenerator.py layout with nonzero f_rest"""
+    n = len(means)
+    hdr = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\n" % n +
+           "".join(f"property float {p}\n" for p in ["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2"]) +
+           "".join(f"property float f_rest_{k}\n" for k in range(45)) +
+           "property float opacity\nproperty float scale_0\nproperty float scale_1\nproperty float scale_2\n"
+           "property float rot_0\nproperty float rot_1\nproperty float rot_2\nproperty float rot_3\nend_header\n")
+    rec = np.zeros((n, 62), np.float32)
+    rec[:, 0:3] = means
+    rec[:, 6:9] = f_dc
+    rec[:, 9:54] = f_rest
+    rec[:, 54] = logit
+    rec[:, 55:58] = log_scale
+    rec[:, 58:62] = rot
+    with open(path, "wb") as f:
+        f.write(hdr.encode())
+        f.write(rec.tobytes())
+
+
+def sh_scene(n=10000, seed=7):
+    means, rot, sc, op, col = c2_scene(n)
+    rng = np.random.default_rng(seed)
+    f_rest = rng.normal(0, 0.3, (n, 45)).astype(np.float32)
+    return means, col, f_rest, np.log(op / (1 - op)).astype(np.float32), np.log(sc).astype(np.float32), rot
+
+
+def test_ply_sh_roundtrip(tmp_path):
+    means, f_dc, f_rest, logit, log_scale, rot = sh_scene(300)
+    p = str(tmp_path / "sh.ply")
+    write_ply_with_sh(p, means, f_dc, f_rest, logit, log_scale, rot)
+    d, r = g.load_ply_sh(p, 300)
+    assert np.array_equal(d, f_dc) and np.array_equal(r, f_rest)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
+def test_sh_frame_matches_oracle(tmp_path, flags):
+    from oracle import oracle as O
+    O.build()
+    W, H = 512, 384
+    ctx = g.Context(0)
+    means, f_dc, f_rest, logit, log_scale, rot = sh_scene()
+    p = str(tmp_path / "sh.ply")
+    write_ply_with_sh(p, means, f_dc, f_rest, logit, log_scale, rot)
+    sp = g.Splats(p, W, H, ctx=ctx, sh=True)
+    u = g.main_camera(W, H).uniforms()
+    sp.flags = flags | g.GS_FLAG_SH
+    sp.render_uniforms(u)
+    img = sp.texture()
+    cols = O.sh_colours(sp.means3D, f_dc, f_rest, np.array(u.view, np.float32), np.ones(sp.numSplats, np.uint8),
+                        sp.colours)
+    ref = O.render(sp.means3D, sp.covarianceMatrices, sp.opacities, cols, u, flags=flags, stages=False)
+    assert np.array_equal(img.reshape(-1), ref["image"].reshape(-1))
+    # view dependence: another pose changes colours, still bit-exact
+    cam = g.main_camera(W, H)
+    cam.rotateRight(15.0)
+    u2 = cam.uniforms()
+    sp.render_uniforms(u2)
+    cols2 = O.sh_colours(sp.means3D, f_dc, f_rest, np.array(u2.view, np.float32), np.ones(sp.numSplats, np.uint8),
+                         sp.colours)
+    ref2 = O.render(sp.means3D, sp.covarianceMatrices, sp.opacities, cols2, u2, flags=flags, stages=False)
+    assert np.array_equal(sp.texture().reshape(-1), ref2["image"].reshape(-1))
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_sh_zero_rest_is_reference_colour(tmp_path):
+    W, H = 384, 256
+    ctx = g.Context(0)
+    means, f_dc, f_rest, logit, log_scale, rot = sh_scene(5000)
+    f_dc = np.abs(f_dc)  # (0.5 + SH_C0 f_dc) >= 0: the SH path's clamp is inactive
+    p = str(tmp_path / "sh0.ply")
+    write_ply_with_sh(p, means, f_dc, np.zeros_like(f_rest), logit, log_scale, rot)
+    sp = g.Splats(p, W, H, ctx=ctx, sh=True)
+    u = g.main_camera(W, H).uniforms()
+    sp.render_uniforms(u)
+    base = sp.texture()
+    sp.flags = g.GS_FLAG_SH
+    sp.render_uniforms(u)
+    assert np.array_equal(base, sp.texture())
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_sh_flag_needs_sh(tmp_path):
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene(100)
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, 64, 64, ctx=ctx)
+    sp.flags = g.GS_FLAG_SH
+    with pytest.raises(g.GsError, match="no SH"):
+        sp.render_uniforms(g.main_camera(64, 64).uniforms())
+    ctx.close()
