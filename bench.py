@@ -172,6 +172,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--clean", action="store_true", help="GS_FLAG_CLEAN: reference quirks fixed")
     ap.add_argument("--fast-exp", action="store_true", help="GS_FLAG_FAST_EXP: hardware exp in the blend")
+    ap.add_argument("--sh", action="store_true", help="GS_FLAG_SH: degree-3 SH colours (SURVEY f3, beyond the "
+                    "reference; seeded synthetic f_rest)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -182,9 +184,15 @@ def main():
 
     cfg = CONFIGS[args.config]
     W, H = cfg["W"], cfg["H"]
-    flags = (g.GS_FLAG_CLEAN if args.clean else 0) | (g.GS_FLAG_FAST_EXP if args.fast_exp else 0)
+    flags = ((g.GS_FLAG_CLEAN if args.clean else 0) | (g.GS_FLAG_FAST_EXP if args.fast_exp else 0) |
+             (g.GS_FLAG_SH if args.sh else 0))
     ctx = g.Context(local)
     sp, data_desc = load_scene(args.config, W, H, ctx, flags)
+    if args.sh:
+        rng = np.random.default_rng(4242)
+        f_dc = ((sp.colours[:, :3] / 255.0 - 0.5) / 0.28209479177387814).astype(np.float32)
+        sp.set_sh(f_dc, rng.normal(0, 0.1, (sp.numSplats, 45)).astype(np.float32))
+        data_desc += "; seeded synthetic f_rest N(0, 0.1^2)"
     u = camera_for_rank(W, H, rank).uniforms()
 
     for _ in range(args.warmup):
@@ -268,7 +276,8 @@ def main():
             "dtype": "f32",
             "data": data_desc,
             "config": {"workload": cfg["desc"] + (" (clean mode)" if args.clean else " (ref mode)") +
-                       (", fast exp" if args.fast_exp else ", defined exp"),
+                       (", fast exp" if args.fast_exp else ", defined exp") +
+                       (", SH degree 3 (beyond the reference)" if args.sh else ""),
                        "splats": N, "width": W, "height": H, "views_per_gpu": 1,
                        "parallelism": f"replicas x{world} (independent views, no collective)"},
             "frame": {"V": V, "D": D, "E": E, "D_over_N": round(D / max(N, 1), 4),
