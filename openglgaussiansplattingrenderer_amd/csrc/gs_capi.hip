@@ -977,18 +977,40 @@ int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
 
 int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset) {
     if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
-    GS_HIP(ctx, hipMemcpyAsync(out, ctx->draw_stats, 128, hipMemcpyDeviceToHost, ctx->stream));
+    if (int rc = gs_sync(ctx)) return rc;
+    std::vector<uint32_t> tr((size_t)gs::kDrawTraceBlocks * gs::kDrawTraceWords);
+    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, gs::kDrawStatsBytes, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::memset(out, 0, 16 * sizeof(uint64_t));
+    for (int b = 0; b < gs::kDrawTraceBlocks; ++b) {
+        const uint32_t *r = tr.data() + (size_t)b * gs::kDrawTraceWords;
+        if (r[1] == 0 && r[0] == 0) continue;  // block not drawn (or beyond its tile)
+        const uint64_t cyc = (uint64_t)(uint32_t)(r[1] - r[0]);
+        out[0] += 1;
+        out[1] += r[2];
+        out[2] += r[3];
+        out[3] += r[7];
+        out[4] = std::max<uint64_t>(out[4], r[2]);
+        out[5] = std::max<uint64_t>(out[5], r[3]);
+        out[6] = std::max<uint64_t>(out[6], cyc);
+        out[7] += cyc;
+        out[8] += r[4];
+        out[9] += r[5];
+        out[10] += r[6];
+    }
     return GS_OK;
 }
 
 int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks) {
     if (!ctx || !out || max_blocks < 0) return set_error(ctx, GS_ERR_INVALID, "bad argument");
+    if (int rc = gs_sync(ctx)) return rc;
     const int n = std::min(max_blocks, gs::kDrawTraceBlocks);
-    GS_HIP(ctx, hipMemcpyAsync(out, (const char *)ctx->draw_stats + 128, (size_t)n * 16, hipMemcpyDeviceToHost,
-                               ctx->stream));
+    std::vector<uint32_t> tr((size_t)n * gs::kDrawTraceWords);
+    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int b = 0; b < n; ++b)
+        for (int k = 0; k < 4; ++k) out[4 * (size_t)b + k] = tr[(size_t)b * gs::kDrawTraceWords + k];
     return n;
 }
 

@@ -119,10 +119,12 @@ void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t 
 constexpr int kPlyFloats = 62;
 void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, int n, float *soa, float4 *colour);
 
-// GS_FLAG_DRAW_STATS buffer: 16 counters, then per block {start, end} (s_memrealtime, 100 MHz),
-// iterations, survivors
+// GS_FLAG_DRAW_STATS buffer: per block (launch order) kDrawTraceWords uint32: start, end
+// (s_memrealtime, 100 MHz), steps, survivors, (wave, survivor) steps, steps with a needing
+// pixel, (pixel, survivor) needs, list entries in range; the host aggregates (gs_draw_stats)
 constexpr int kDrawTraceBlocks = 65536;
-constexpr size_t kDrawStatsBytes = 128 + (size_t)kDrawTraceBlocks * 16;
+constexpr int kDrawTraceWords = 8;
+constexpr size_t kDrawStatsBytes = (size_t)kDrawTraceBlocks * kDrawTraceWords * 4;
 
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
                  const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats, hipEvent_t start,

@@ -822,26 +822,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 1]);
     if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(s_col[4 * lane + 2]);
     if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 3]);
-    if (STATS && lane == 0) {
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(), cyc = t1 - st_t0;
+    if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         if (L < kDrawTraceBlocks) {
-            uint32_t *tr = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(stats) + 128) + 4 * L;
+            uint32_t *tr = reinterpret_cast<uint32_t *>(stats) + kDrawTraceWords * L;
             tr[0] = (uint32_t)st_t0;
             tr[1] = (uint32_t)t1;
             tr[2] = (uint32_t)st_iter;
             tr[3] = (uint32_t)st_surv;
+            tr[4] = (uint32_t)st_kit;
+            tr[5] = (uint32_t)st_anyneed;
+            tr[6] = (uint32_t)st_pxneed;
+            tr[7] = (uint32_t)max(0, end - start);
         }
-        atomicAdd(&stats[0], 1ull);
-        atomicAdd(&stats[1], st_iter);
-        atomicAdd(&stats[2], st_surv);
-        atomicAdd(&stats[3], (unsigned long long)max(0, end - start));
-        atomicMax(&stats[4], st_iter);
-        atomicMax(&stats[5], st_surv);
-        atomicMax(&stats[6], cyc);
-        atomicAdd(&stats[7], cyc);
-        atomicAdd(&stats[8], st_kit);
-        atomicAdd(&stats[9], st_anyneed);
-        atomicAdd(&stats[10], st_pxneed);
     }
 }
 
