@@ -81,6 +81,23 @@ __device__ __forceinline__ float exp_defined(float x) {
     return p * u2f((uint32_t)(k + 127) << 23);
 }
 
+// exp_defined on a blend event's power (x <= 0 or NaN): the same bits for every such x (its
+// underflow branch as a select; the x > 80 clamp cannot apply), without a branch
+__device__ __forceinline__ float exp_defined_event(float x) {
+    const float kf = rintf(x * 1.44269504088896341f);
+    float r = __builtin_fmaf(-kf, 0.693359375f, x);
+    r = __builtin_fmaf(-kf, -2.12194440e-4f, r);
+    float t = __builtin_fmaf(0.00138888892f, r, 0.00833333377f);
+    t = __builtin_fmaf(t, r, 0.0416666679f);
+    t = __builtin_fmaf(t, r, 0.166666672f);
+    t = __builtin_fmaf(t, r, 0.5f);
+    t = __builtin_fmaf(t, r, 1.0f);
+    const float p = __builtin_fmaf(t, r, 1.0f);
+    const int k = (int)kf;
+    const float v = p * u2f((uint32_t)(k + 127) << 23);
+    return (x >= -80.0f) ? v : 0.0f;
+}
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // inclusive wave scan (wave64)
@@ -588,10 +605,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
                                              const float4 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
                                              uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
-    __shared__ float4 s_col[256];    // pixel state, pixel id = 4*lane + slot
-    __shared__ uint32_t s_done[64];  // per lane: one done byte per slot
-    __shared__ float s_epow[256];    // one survivor's blend events: power ...
-    __shared__ uint8_t s_epix[256];  // ... and pixel id (split: 5.5 KB of LDS per wave -> 7 waves/SIMD)
+    // pixel state, pixel id = 4*lane + slot; a pixel is done (:129-133) iff its w >= 0.99 (pixels
+    // outside the image start at w = 1)
+    __shared__ float4 s_col[256];
+    // one survivor's blend events: power and pixel id (split), entries 256 + lane take the
+    // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
+    __shared__ float s_epow[256 + 64];
+    __shared__ uint8_t s_epix[256 + 64];
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
@@ -643,13 +663,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    s_done[lane] = (d00 ? 1u : 0u) | (d10 ? 0x100u : 0u) | (d01 ? 0x10000u : 0u) | (d11 ? 0x1000000u : 0u);
+    for (int k = 0; k < 4; ++k) {
+        const bool dk = k == 0 ? d00 : k == 1 ? d10 : k == 2 ? d01 : d11;
+        s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
+    }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
     const int jmax = max(end - 1, 0);
-    bool all_done = __all(d00 && d10 && d01 && d11);
+    // done pixels as uniform lane masks per slot (scalar loop state; refreshed from s_col only
+    // after a survivor saturated a pixel)
+    uint64_t D0 = ballot(d00), D1 = ballot(d10), D2 = ballot(d01), D3 = ballot(d11);
+    bool all_done = (D0 & D1 & D2 & D3) == ~0ull;
+    float ninf_v = -__builtin_inff();
+    // v_cndmask on a uniform mask: m's lane bit set -> -inf, else r
+    auto mask_ninf = [&](float r, uint64_t m) {
+        float o;
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(ninf_v), "s"(m));
+        return o;
+    };
 
     // The list streams through a four-stage pipeline, one 64-entry chunk per step; chunk c:
     //   step c-3: index load (coalesced)            step c-2: box gather
@@ -711,11 +743,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             const f32x2 r0 = h * (ax + f32x2{cy.x, cy.x}) - bxd * f32x2{dy.x, dy.x};  // (p00, p10)
             const f32x2 r1 = h * (ax + f32x2{cy.y, cy.y}) - bxd * f32x2{dy.y, dy.y};  // (p01, p11)
             // a saturated pixel's power is replaced by -inf, which never needs a blend
-            const float ninf = -__builtin_inff();
-            const float p00 = d00 ? ninf : r0.x;
-            const float p10 = d10 ? ninf : r0.y;
-            const float p01 = d01 ? ninf : r1.x;
-            const float p11 = d11 ? ninf : r1.y;
+            const float p00 = mask_ninf(r0.x, D0);
+            const float p10 = mask_ninf(r0.y, D1);
+            const float p01 = mask_ninf(r1.x, D2);
+            const float p11 = mask_ninf(r1.y, D3);
             // :118-126 (power > 0 -> continue), plus the exact pre-exp skip (power < thr)
             const bool n00 = !(p00 > 0.0f) && !(p00 < thr);
             const bool n10 = !(p10 > 0.0f) && !(p10 < thr);
@@ -740,53 +771,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             auto below = [&](uint64_t m, uint32_t base0) {
                 return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
             };
-            if (n00) {
-                const uint32_t e = below(b0, 0);
+            // every lane writes each slot: lanes without that event into their own spare entry
+            const uint32_t spare = 256u + (uint32_t)lane;
+            {
+                const uint32_t e = n00 ? below(b0, 0) : spare;
                 s_epow[e] = p00;
                 s_epix[e] = (uint8_t)(4 * lane + 0);
             }
-            if (n10) {
-                const uint32_t e = below(b1, e0);
+            {
+                const uint32_t e = n10 ? below(b1, e0) : spare;
                 s_epow[e] = p10;
                 s_epix[e] = (uint8_t)(4 * lane + 1);
             }
-            if (n01) {
-                const uint32_t e = below(b2, e0 + e1);
+            {
+                const uint32_t e = n01 ? below(b2, e0 + e1) : spare;
                 s_epow[e] = p01;
                 s_epix[e] = (uint8_t)(4 * lane + 2);
             }
-            if (n11) {
-                const uint32_t e = below(b3, e0 + e1 + e2);
+            {
+                const uint32_t e = n11 ? below(b3, e0 + e1 + e2) : spare;
                 s_epow[e] = p11;
                 s_epix[e] = (uint8_t)(4 * lane + 3);
             }
             wave_lds_sync();
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
+            uint32_t sat = 0;  // max bits of the w written (w >= 0: ordered as the floats)
             for (uint32_t e = lane; e < nev; e += 64) {
+                // straight line: the pixel's state is loaded with the event, before the exp
                 const uint32_t pix = s_epix[e];
                 const float power = s_epow[e];
-                const float ex = FAST_EXP ? __expf(power) : exp_defined(power);
-                const float alpha = fminf(0.99f, ex * o);
-                if (alpha < 1.0f / 255.0f) continue;
-                // alphaBlend :59-67
                 float4 col = s_col[pix];
+                const float ex = FAST_EXP ? __expf(power) : exp_defined_event(power);
+                const float alpha = fminf(0.99f, ex * o);
+                const bool take = !(alpha < 1.0f / 255.0f);
+                // alphaBlend :59-67
                 const float remaining = 1.0f - col.w;
                 const float aT = alpha * remaining;
-                col.x = col.x + r * aT;
-                col.y = col.y + g * aT;
-                col.z = col.z + bl * aT;
-                col.w = col.w + aT;
+                col.x = take ? col.x + r * aT : col.x;
+                col.y = take ? col.y + g * aT : col.y;
+                col.z = take ? col.z + bl * aT : col.z;
+                col.w = take ? col.w + aT : col.w;
                 s_col[pix] = col;
-                if (col.w >= 0.99f) reinterpret_cast<uint8_t *>(s_done)[pix] = 1;  // :129-133
+                sat = max(sat, __float_as_uint(col.w));  // :129-133
             }
-            wave_lds_sync();
-            const uint32_t dm = s_done[lane];
-            d00 = (dm & 0xffu) != 0;
-            d10 = (dm & 0xff00u) != 0;
-            d01 = (dm & 0xff0000u) != 0;
-            d11 = (dm & 0xff000000u) != 0;
-            all_done = __all(d00 && d10 && d01 && d11);  // every pixel saturated
+            if (ballot(sat >= __float_as_uint(0.99f))) {  // uniform, rare: a pixel saturated -- refresh the done masks
+                wave_lds_sync();
+                D0 = ballot(s_col[4 * lane + 0].w >= 0.99f);
+                D1 = ballot(s_col[4 * lane + 1].w >= 0.99f);
+                D2 = ballot(s_col[4 * lane + 2].w >= 0.99f);
+                D3 = ballot(s_col[4 * lane + 3].w >= 0.99f);
+                all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
+            }
+            wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
         }
     };
 

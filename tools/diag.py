@@ -1,5 +1,5 @@
 """Diagnostics on the GPU box: per-stage times and blend work counters for the C3/C4 frames
-in each mode.  python tools/diag.py [c3|c4] [frames]"""
+in each mode.  python tools/diag.py [c3|c4] [frames] [mode,mode,...]"""
 import os
 import sys
 import time
@@ -20,7 +20,10 @@ print(f"scene up in {time.time() - t:.1f}s", flush=True)
 u = g.main_camera(W, H).uniforms()
 variants = [("ref", 0), ("ref+fast", g.GS_FLAG_FAST_EXP), ("clean", g.GS_FLAG_CLEAN),
             ("clean+fast", g.GS_FLAG_CLEAN | g.GS_FLAG_FAST_EXP), ("nocull", g.GS_FLAG_NO_CULL)]
+only = sys.argv[3].split(",") if len(sys.argv) > 3 else None
 for name, fl in variants:
+    if only and name not in only:
+        continue
     sp.flags = fl | g.GS_FLAG_DRAW_STATS
     sp.render_uniforms(u)
     ctx.draw_stats(reset=True)
