@@ -1011,8 +1011,7 @@ int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks) {
     std::vector<uint32_t> tr((size_t)n * gs::kDrawTraceWords);
     GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (int b = 0; b < n; ++b)
-        for (int k = 0; k < 4; ++k) out[4 * (size_t)b + k] = tr[(size_t)b * gs::kDrawTraceWords + k];
+    std::memcpy(out, tr.data(), tr.size() * 4);
     return n;
 }
 

@@ -267,8 +267,10 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             }
         } while (false);
         // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
-        // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends), NaN never skips
-        const float thr = -logf(255.0f * co.w) - 1.0e-3f;
+        // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
+        // becomes -inf, which never skips
+        float thr = -logf(255.0f * co.w) - 1.0e-3f;
+        if (thr != thr) thr = -__builtin_inff();
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
         if (P.sh && rc.y >= 0) {  // GS_FLAG_SH: this frame's colour of a splat that has entries
             float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
@@ -599,8 +601,18 @@ __device__ __forceinline__ uint64_t ballot(bool b) { return __builtin_amdgcn_bal
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// the draw's lane-held copy of a SplatDraw record (without its pad)
+// (read as whole 16-byte aligned records: 28 and 12 bytes, dwordx4 + dwordx3 / dwordx3)
+struct alignas(16) SurvData {
+    float mx, my, a, b, c, o, thr;
+};
+struct alignas(16) SurvRgb {
+    float x, y, z;
+};
+static_assert(offsetof(SplatDraw, thr) == offsetof(SurvData, thr), "SurvData mirrors SplatDraw");
+
 template <bool FAST_EXP, bool STATS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
                                              const float4 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
@@ -668,6 +680,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
         s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
+    unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_t64 = 0;
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
     const int jmax = max(end - 1, 0);
@@ -675,13 +688,66 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     // after a survivor saturated a pixel)
     uint64_t D0 = ballot(d00), D1 = ballot(d10), D2 = ballot(d01), D3 = ballot(d11);
     bool all_done = (D0 & D1 & D2 & D3) == ~0ull;
-    float ninf_v = -__builtin_inff();
-    // v_cndmask on a uniform mask: m's lane bit set -> -inf, else r
-    auto mask_ninf = [&](float r, uint64_t m) {
-        float o;
-        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(o) : "v"(r), "v"(ninf_v), "s"(m));
+    // v_cndmask on a uniform mask: m's lane bit set -> t, else f
+    auto sel_u32 = [](uint32_t f, uint32_t t, uint64_t m) {
+        uint32_t o;
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(o) : "v"(f), "v"(t), "s"(m));
         return o;
     };
+    // does a pixel of power p need the exp / blend path?  :118-126 continue on p > 0, plus the
+    // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr, 0) == p or unordered (one
+    // compare).  For thr > 0 (opacity < ~1/255) it also admits p in [0, thr], where alpha is
+    // below 1/255 (the margin in thr), so those events never blend either.
+    auto needs = [](float p, float thr) {
+        return !__builtin_islessgreater(__builtin_amdgcn_fmed3f(p, thr, 0.0f), p);
+    };
+    auto below = [](uint64_t m, uint32_t base0) {  // base0 + set bits of m below this lane
+        return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
+    };
+    // the cull rectangle: the sub-block, then the bounding box of its active pixels (a done
+    // pixel never blends, so a splat missing every active pixel is skipped exactly)
+    float rx0 = bx0, rx1 = bx1, ry0 = by0, ry1 = by1;
+
+    // Sparse phase: once at most 64 pixels are active, each lane takes one of them (its state
+    // in registers for the survivors of a chunk) and a survivor costs one power / exp / blend
+    // per lane and no LDS traffic.  Lanes >= nact name lane nact-1's pixel and stay inactive.
+    bool sparse = false;
+    uint64_t SA = 0;   // lanes whose pixel is active
+    uint32_t spix = 0, nact = 0;
+    auto go_sparse = [&]() {
+        wave_lds_sync();
+        const uint64_t A0 = ~D0, A1 = ~D1, A2 = ~D2, A3 = ~D3;
+        const uint32_t a0 = (uint32_t)__popcll(A0), a1 = (uint32_t)__popcll(A1), a2 = (uint32_t)__popcll(A2);
+        nact = a0 + a1 + a2 + (uint32_t)__popcll(A3);
+        const uint32_t spare = 256u + (uint32_t)lane;
+        s_epix[((A0 >> lane) & 1) ? below(A0, 0) : spare] = (uint8_t)(4 * lane + 0);
+        s_epix[((A1 >> lane) & 1) ? below(A1, a0) : spare] = (uint8_t)(4 * lane + 1);
+        s_epix[((A2 >> lane) & 1) ? below(A2, a0 + a1) : spare] = (uint8_t)(4 * lane + 2);
+        s_epix[((A3 >> lane) & 1) ? below(A3, a0 + a1 + a2) : spare] = (uint8_t)(4 * lane + 3);
+        wave_lds_sync();
+        spix = s_epix[min((uint32_t)lane, nact - 1)];
+        SA = nact >= 64 ? ~0ull : ((1ull << nact) - 1);
+        const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
+        const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
+        float mnx = sfx, mxx = sfx, mny = sfy, mxy = sfy;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            mnx = fminf(mnx, __shfl_xor(mnx, o, 64));
+            mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
+            mny = fminf(mny, __shfl_xor(mny, o, 64));
+            mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64));
+        }
+        auto uni = [](float v) {  // uniform -> scalar register
+            return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+        };
+        rx0 = uni(mnx);
+        rx1 = uni(mxx);
+        ry0 = uni(mny);
+        ry1 = uni(mxy);
+        sparse = true;
+    };
+    // blocks with few pixels in the image start sparse
+    if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) go_sparse();
 
     // The list streams through a four-stage pipeline, one 64-entry chunk per step; chunk c:
     //   step c-3: index load (coalesced)            step c-2: box gather
@@ -694,8 +760,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
     uint32_t Vi[2], Vb[2];      // indices: as loaded / riding with the box gather
     float4 Bx[2];               // boxes
     uint64_t K[2];              // survivors of the box test (then of the exact cull)
-    SplatDraw Dd[2];            // survivor data (lane-held; other lanes hold copies)
-    float4 Dc[2];               // survivor colour
+    SurvData Dd[2];             // survivor data (lane-held; other lanes hold copies)
+    SurvRgb Dc[2];              // survivor colour
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -709,22 +775,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
         vb = v;
         bx = *at(cullbox, v << 4);
     };
-    auto test_and_gather = [&](int cbase, uint32_t v, const float4 &bx, uint64_t &keep, SplatDraw &d,
-                               float4 &c) {
+    auto test_and_gather = [&](int cbase, uint32_t v, const float4 &bx, uint64_t &keep, SurvData &d,
+                               SurvRgb &c) {
         // bitwise, not short-circuit: no branch around the compares
         const bool in = (cbase + lane < end) &
-                        (!cull | ((bx.x <= bx1) & (bx.y >= bx0) & (bx.z <= by1) & (bx.w >= by0)));
+                        (!cull | ((bx.x <= rx1) & (bx.y >= rx0) & (bx.z <= ry1) & (bx.w >= ry0)));
         keep = ballot(in);
         // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
         const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
         const uint32_t idx = in ? v : first;
-        d = *at(sd, idx << 5);
-        c = *at(colour, idx << 4);
+        // the 7 used floats of the SplatDraw record and rgb of the colour
+        d = *at(reinterpret_cast<const SurvData *>(sd), idx << 5);
+        c = *at(reinterpret_cast<const SurvRgb *>(colour), idx << 4);
     };
-    auto blend = [&](uint64_t keep, const SplatDraw &d, const float4 &c) {
+    // dense phase: every survivor's power at all 256 pixels, its blend events compacted into
+    // LDS and run one per lane.  Returns true when the block turns sparse (keep: the chunk's
+    // survivors left for the sparse phase).
+    auto blend_dense = [&](uint64_t &keep, const SurvData &d, const SurvRgb &c) {
         // exact cull of the survivors (uniform keep mask)
         if (cull) keep &= ~ballot(((keep >> lane) & 1ull) &&
-                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, bx0, bx1, by0, by1));
+                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         while (keep && !all_done) {
             const int src = __builtin_ctzll(keep);
@@ -742,54 +812,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             const f32x2 h = f32x2{-0.5f, -0.5f};
             const f32x2 r0 = h * (ax + f32x2{cy.x, cy.x}) - bxd * f32x2{dy.x, dy.x};  // (p00, p10)
             const f32x2 r1 = h * (ax + f32x2{cy.y, cy.y}) - bxd * f32x2{dy.y, dy.y};  // (p01, p11)
-            // a saturated pixel's power is replaced by -inf, which never needs a blend
-            const float p00 = mask_ninf(r0.x, D0);
-            const float p10 = mask_ninf(r0.y, D1);
-            const float p01 = mask_ninf(r1.x, D2);
-            const float p11 = mask_ninf(r1.y, D3);
-            // :118-126 (power > 0 -> continue), plus the exact pre-exp skip (power < thr)
-            const bool n00 = !(p00 > 0.0f) && !(p00 < thr);
-            const bool n10 = !(p10 > 0.0f) && !(p10 < thr);
-            const bool n01 = !(p01 > 0.0f) && !(p01 < thr);
-            const bool n11 = !(p11 > 0.0f) && !(p11 < thr);
-            // ballots of the bare compares (a ballot of a combined lane bool costs two VALU)
-            const uint64_t b0 = ballot(!(p00 > 0.0f)) & ballot(!(p00 < thr));
-            const uint64_t b1 = ballot(!(p10 > 0.0f)) & ballot(!(p10 < thr));
-            const uint64_t b2 = ballot(!(p01 > 0.0f)) & ballot(!(p01 < thr));
-            const uint64_t b3 = ballot(!(p11 > 0.0f)) & ballot(!(p11 < thr));
+            const float p00 = r0.x, p10 = r0.y, p01 = r1.x, p11 = r1.y;
+            // events: needing pixels that are not done
+            const uint64_t b0 = ballot(needs(p00, thr)) & ~D0;
+            const uint64_t b1 = ballot(needs(p10, thr)) & ~D1;
+            const uint64_t b2 = ballot(needs(p01, thr)) & ~D2;
+            const uint64_t b3 = ballot(needs(p11, thr)) & ~D3;
             const uint32_t e0 = (uint32_t)__popcll(b0), e1 = (uint32_t)__popcll(b1);
             const uint32_t e2 = (uint32_t)__popcll(b2), e3 = (uint32_t)__popcll(b3);
             const uint32_t nev = e0 + e1 + e2 + e3;
             if (STATS) {
                 ++st_kit;
+                const int active = 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3);
+                st_kit64 += active <= 64 ? 1 : 0;
+                st_kit128 += active <= 128 ? 1 : 0;
+                st_ev64 += active <= 64 ? nev : 0;
+                if (active <= 64 && st_t64 == 0) st_t64 = __builtin_amdgcn_s_memrealtime() - st_t0;
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
             }
             if (nev == 0) continue;  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
-            // v_mbcnt); each pixel occurs at most once, so the events are independent
-            auto below = [&](uint64_t m, uint32_t base0) {
-                return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
-            };
-            // every lane writes each slot: lanes without that event into their own spare entry
+            // v_mbcnt); each pixel occurs at most once, so the events are independent.  Every
+            // lane writes each slot: lanes without that event into their own spare entry.
             const uint32_t spare = 256u + (uint32_t)lane;
             {
-                const uint32_t e = n00 ? below(b0, 0) : spare;
+                const uint32_t e = sel_u32(spare, below(b0, 0), b0);
                 s_epow[e] = p00;
                 s_epix[e] = (uint8_t)(4 * lane + 0);
             }
             {
-                const uint32_t e = n10 ? below(b1, e0) : spare;
+                const uint32_t e = sel_u32(spare, below(b1, e0), b1);
                 s_epow[e] = p10;
                 s_epix[e] = (uint8_t)(4 * lane + 1);
             }
             {
-                const uint32_t e = n01 ? below(b2, e0 + e1) : spare;
+                const uint32_t e = sel_u32(spare, below(b2, e0 + e1), b2);
                 s_epow[e] = p01;
                 s_epix[e] = (uint8_t)(4 * lane + 2);
             }
             {
-                const uint32_t e = n11 ? below(b3, e0 + e1 + e2) : spare;
+                const uint32_t e = sel_u32(spare, below(b3, e0 + e1 + e2), b3);
                 s_epow[e] = p11;
                 s_epix[e] = (uint8_t)(4 * lane + 3);
             }
@@ -797,7 +860,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
             uint32_t sat = 0;  // max bits of the w written (w >= 0: ordered as the floats)
-            for (uint32_t e = lane; e < nev; e += 64) {
+            auto event = [&](uint32_t e) {
                 // straight line: the pixel's state is loaded with the event, before the exp
                 const uint32_t pix = s_epix[e];
                 const float power = s_epow[e];
@@ -814,7 +877,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
                 col.w = take ? col.w + aT : col.w;
                 s_col[pix] = col;
                 sat = max(sat, __float_as_uint(col.w));  // :129-133
-            }
+            };
+            if ((uint32_t)lane < nev) event(lane);
+            if (nev > 64)  // uniform, rare: more events than lanes
+                for (uint32_t e = lane + 64; e < nev; e += 64) event(e);
             if (ballot(sat >= __float_as_uint(0.99f))) {  // uniform, rare: a pixel saturated -- refresh the done masks
                 wave_lds_sync();
                 D0 = ballot(s_col[4 * lane + 0].w >= 0.99f);
@@ -822,9 +888,60 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
                 D2 = ballot(s_col[4 * lane + 2].w >= 0.99f);
                 D3 = ballot(s_col[4 * lane + 3].w >= 0.99f);
                 all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
+                if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) {
+                    wave_lds_sync();
+                    return true;
+                }
             }
             wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
         }
+        return false;
+    };
+
+    // sparse phase (see go_sparse): one pixel per lane, state in registers
+    auto blend_sparse = [&](uint64_t keep, const SurvData &d, const SurvRgb &c) {
+        if (cull) keep &= ~ballot(((keep >> lane) & 1ull) &&
+                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
+        if (STATS) st_surv += __popcll(keep);
+        if (!keep) return;  // uniform
+        float4 pc = s_col[spix];
+        const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
+        const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
+        while (keep && !all_done) {
+            const int src = __builtin_ctzll(keep);
+            keep &= keep - 1;
+            const float mx = rl(d.mx, src), my = rl(d.my, src);
+            const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
+            const float thr = rl(d.thr, src);
+            // :111-116, the same op sequence as the packed form below
+            const float dx = sfx - mx, dy = sfy - my;
+            const float p = -0.5f * ((ca * dx) * dx + (cc * dy) * dy) - (cbv * dx) * dy;
+            const uint64_t nb = SA & ballot(needs(p, thr));
+            if (STATS) {
+                ++st_kit;
+                ++st_kit64;
+                ++st_kit128;
+                st_anyneed += nb ? 1 : 0;
+                st_pxneed += __popcll(nb);
+                st_ev64 += __popcll(nb);
+            }
+            if (!nb) continue;  // uniform
+            const float o = rl(d.o, src);
+            const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
+            const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
+            const float alpha = fminf(0.99f, ex * o);
+            const bool take = ((nb >> lane) & 1) & !(alpha < 1.0f / 255.0f);
+            // alphaBlend :59-67
+            const float aT = alpha * (1.0f - pc.w);
+            pc.x = take ? pc.x + r * aT : pc.x;
+            pc.y = take ? pc.y + g * aT : pc.y;
+            pc.z = take ? pc.z + bl * aT : pc.z;
+            pc.w = take ? pc.w + aT : pc.w;
+            SA &= ~ballot(pc.w >= 0.99f);  // :129-133
+            all_done = SA == 0;
+        }
+        if ((uint32_t)lane < nact) s_col[spix] = pc;  // distinct pixels
+        wave_lds_sync();
     };
 
     // prologue: chunk 0 box-gathered, chunk 1 index-loaded ... see the stage table above
@@ -838,14 +955,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
         test_and_gather(base, Vb[0], Bx[0], K[0], Dd[0], Dc[0]);   // chunk 0: data in flight
         gather_box(Vi[1], Vb[1], Bx[1]);                     // chunk 1: box in flight
         // chunk c's stages use slot c & 1 for data, (c + 1) & 1 for the box and c & 1 for the
-        // index; step c (slot u = c & 1) runs:
-        auto step = [&](auto U) {
+        // index; step c (slot u = c & 1) issues the loads of chunks c+1..c+3, then blends c
+        auto loads = [&](auto U) {
             constexpr int u = decltype(U)::value, w = u ^ 1;
             load_idx(base + 192, Vi[w]);                           // chunk c+3
             gather_box(Vi[u], Vb[u], Bx[u]);                       // chunk c+2
             test_and_gather(base + 64, Vb[w], Bx[w], K[w], Dd[w], Dc[w]);   // chunk c+1
             if (STATS) ++st_iter;
-            blend(K[u], Dd[u], Dc[u]);                             // chunk c
+        };
+        auto step = [&](auto U) {
+            constexpr int u = decltype(U)::value;
+            loads(U);
+            // uniform branches; a block that turns sparse mid-chunk leaves the chunk's
+            // remaining survivors in K[u] for the sparse blend
+            if (!sparse && blend_dense(K[u], Dd[u], Dc[u])) go_sparse();
+            if (sparse) blend_sparse(K[u], Dd[u], Dc[u]);
             base += 64;
             return base < end && !all_done;
         };
@@ -871,6 +995,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void k_
             tr[5] = (uint32_t)st_anyneed;
             tr[6] = (uint32_t)st_pxneed;
             tr[7] = (uint32_t)max(0, end - start);
+            tr[8] = (uint32_t)st_kit64;
+            tr[9] = (uint32_t)st_kit128;
+            tr[10] = (uint32_t)st_ev64;
+            tr[11] = (uint32_t)st_t64;
         }
     }
 }

@@ -67,8 +67,10 @@ class Context:
                     wave_steps=int(a[8]), steps_any_need=int(a[9]), pixel_needs=int(a[10]))
 
     def draw_block_trace(self, blocks: int) -> np.ndarray:
-        """[blocks, 4] uint32: start, end (100 MHz ticks), iterations, survivors per draw block."""
-        a = np.zeros((blocks, 4), np.uint32)
+        """[blocks, 12] uint32 per draw block (gs_draw_block_trace): start, end (100 MHz ticks),
+        iterations, survivors, survivor steps, steps with a needing pixel, pixel needs, list
+        entries, steps while <= 64 / <= 128 pixels active, events while <= 64, ticks to <= 64."""
+        a = np.zeros((blocks, 12), np.uint32)
         n = lib().gs_draw_block_trace(self.handle, ptr(a), int(blocks))
         check(n, self.handle)
         return a[:n]

@@ -38,8 +38,28 @@ print("resident blocks at 5% steps:", act)
 o = np.argsort(-d)[:8]
 for i in o:
     print(f"  long block: {d[i]:.1f} us start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]}")
-fit = np.polyfit(np.stack([tr[:, 2], tr[:, 3]], 1).astype(float).T[0], d, 1) if len(tr) > 2 else None
 A = np.stack([tr[:, 2], tr[:, 3], np.ones(len(tr))], 1).astype(float)
 coef, *_ = np.linalg.lstsq(A, d, rcond=None)
 print(f"duration ~ {coef[0]:.3f} us/iteration + {coef[1]:.3f} us/survivor + {coef[2]:.1f} us")
+# event passes: a survivor with k needing pixels runs ceil(k/64) passes; per block only the sum
+A = np.stack([tr[:, 2], tr[:, 5], tr[:, 6] / 64.0, np.ones(len(tr))], 1).astype(float)
+coef, *_ = np.linalg.lstsq(A, d, rcond=None)
+res = d - A @ coef
+print(f"duration ~ {coef[0]:.3f} us/iteration + {coef[1]:.3f} us/needing survivor + {coef[2]:.3f} us/64 events"
+      f" + {coef[3]:.1f} us  (residual rms {res.std():.1f} us)")
+for lo, hi in ((0, 25), (25, 50), (50, 75), (75, 100)):
+    m = (s >= np.percentile(s, lo)) & (s <= np.percentile(s, hi))
+    print(f"  start pct {lo}-{hi}: mean dur {d[m].mean():.1f} us  iters {tr[m, 2].mean():.1f}  need-surv {tr[m, 5].mean():.1f}"
+          f"  events {tr[m, 6].mean():.0f}")
+for i in o:
+    print(f"  long block {i}: {d[i]:.1f} us  steps {tr[i, 4]} needing {tr[i, 5]} events {tr[i, 6]} entries {tr[i, 7]}")
+short = np.argsort(d)[:5]
+for i in short:
+    print(f"  short block {i}: {d[i]:.1f} us  start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]} events {tr[i, 6]}")
+k64, k128, ev64, t64 = tr[:, 8].sum(), tr[:, 9].sum(), tr[:, 10].sum(), tr[:, 11]
+print(f"survivor steps {tr[:, 4].sum()}: with <=64 active px {k64} ({k64 / tr[:, 4].sum():.1%}), <=128 {k128}"
+      f" ({k128 / tr[:, 4].sum():.1%}); events with <=64 active {ev64} ({ev64 / tr[:, 6].sum():.1%})")
+r = t64[t64 > 0] * 0.01
+print(f"blocks reaching <=64 active: {len(r)}; time to reach it / duration: "
+      f"{np.median(t64[t64 > 0] * 0.01 / d[t64 > 0]):.2f} (median)")
 print("counters:", st)
