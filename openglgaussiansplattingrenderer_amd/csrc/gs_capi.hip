@@ -705,10 +705,14 @@ int enqueue_emit(gs_ctx *ctx) {
 }
 
 // E entries, or (count != null) min(E, count[0] + count[1]) read on the device
-int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count) {
+// with_bins: the tile bins (gs_compute_bins' output) come from the sort's own histogram read;
+// the bins stage is then empty (its timing event follows the sort's)
+int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false) {
     if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5)))
+                                fev(ctx, 5), with_bins ? ctx->bins : nullptr))
         return set_error(ctx, rc, ctx->err);
+    if (with_bins)
+        if (hipEvent_t e = fev(ctx, 6)) GS_HIP(ctx, hipEventRecord(e, ctx->stream));
     return GS_OK;
 }
 
@@ -780,8 +784,8 @@ int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
                 int out_on_device, gs_frame_stats *stats) {
     int rc;
     if ((rc = gs_preprocess(ctx, scene, u, flags, stats))) return rc;
-    if ((rc = gs_sort(ctx))) return rc;
-    if ((rc = gs_compute_bins(ctx))) return rc;
+    if ((rc = enqueue_sort(ctx, ctx->E, nullptr, true))) return rc;  // gs_sort + gs_compute_bins
+    ctx->stage = 3;
     // src/Splats.cpp:596 draw(width, height, float(width) / 16.f, float(height) / 16.f)
     return gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags, out,
                    out_on_device);
@@ -804,7 +808,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     sl.cap = ctx->e_cap;
     const uint32_t *cnt = ctx->totals;
     int rc;
-    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->e_cap, cnt)) || (rc = enqueue_bins(ctx, ctx->e_cap, cnt)))
+    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->e_cap, cnt, true)))
         return rc;
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
                            out, 1, ctx->e_cap, cnt)))

@@ -66,13 +66,17 @@ struct SortScratch {
     size_t alt_cap = 0;            // elements
     uint32_t *hist = nullptr;      // [256][nb]
     size_t hist_cap = 0;           // elements
-    uint32_t *row_total = nullptr; // [256]
+    uint32_t *row_total = nullptr; // [256], then [16][256] tile counts (zero between sorts)
 };
 
-// n elements, or -- when dev_count is given -- min(n, dev_count[0] + dev_count[1]) read on the
-// device (n is then the capacity the grids are sized for)
+// Stable sort of (key, value) pairs: n elements, or -- when dev_count is given -- min(n,
+// dev_count[0] + dev_count[1]) read on the device (n is then the capacity the grids are sized
+// for).  With bins != null, also the reference's tile bins of the keys (countBins.glsl +
+// prefix: bins[t] = #keys with int(key) <= t) and the longest-first tile order in bins[256..511]
+// (what launch_bins computes), counted during the first pass's histogram read.
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
-               const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+               const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
+               uint32_t *bins = nullptr);
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]

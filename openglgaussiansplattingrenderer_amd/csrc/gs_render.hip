@@ -62,27 +62,11 @@ __device__ __forceinline__ M3 tr3(const M3 &a) {
     return o;
 }
 
-// exp of draw.glsl:122 -- the same definition the oracle states (ora_expf: Cody-Waite +
-// degree-6 Horner polynomial, each step one correctly rounded fma); every operation is
-// IEEE-exact, so CPU == GPU bit for bit.
-__device__ __forceinline__ float exp_defined(float x) {
-    if (!(x >= -80.0f)) return 0.0f;
-    if (x > 80.0f) x = 80.0f;
-    const float kf = rintf(x * 1.44269504088896341f);
-    float r = __builtin_fmaf(-kf, 0.693359375f, x);
-    r = __builtin_fmaf(-kf, -2.12194440e-4f, r);
-    float t = __builtin_fmaf(0.00138888892f, r, 0.00833333377f);
-    t = __builtin_fmaf(t, r, 0.0416666679f);
-    t = __builtin_fmaf(t, r, 0.166666672f);
-    t = __builtin_fmaf(t, r, 0.5f);
-    t = __builtin_fmaf(t, r, 1.0f);
-    const float p = __builtin_fmaf(t, r, 1.0f);
-    const int k = (int)kf;
-    return p * u2f((uint32_t)(k + 127) << 23);
-}
-
-// exp_defined on a blend event's power (x <= 0 or NaN): the same bits for every such x (its
-// underflow branch as a select; the x > 80 clamp cannot apply), without a branch
+// exp of draw.glsl:122 -- the definition the oracle states (ora_expf: Cody-Waite + degree-6
+// Horner polynomial, each step one correctly rounded fma; 0 below -80, clamped at 80); every
+// operation is IEEE-exact, so CPU == GPU bit for bit.  This is that function on the powers a
+// blend event can carry (x <= 0 or NaN, see needs() in k_draw), where it is the same bits
+// with the underflow branch as a select and the clamp inapplicable.
 __device__ __forceinline__ float exp_defined_event(float x) {
     const float kf = rintf(x * 1.44269504088896341f);
     float r = __builtin_fmaf(-kf, 0.693359375f, x);
@@ -695,11 +679,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         return o;
     };
     // does a pixel of power p need the exp / blend path?  :118-126 continue on p > 0, plus the
-    // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr, 0) == p or unordered (one
-    // compare).  For thr > 0 (opacity < ~1/255) it also admits p in [0, thr], where alpha is
-    // below 1/255 (the margin in thr), so those events never blend either.
-    auto needs = [](float p, float thr) {
-        return !__builtin_islessgreater(__builtin_amdgcn_fmed3f(p, thr, 0.0f), p);
+    // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr_e, 0) == p or unordered (one
+    // compare), thr_e = min(thr, 0).  For thr > 0 (opacity < ~1/255) it admits p = +-0 only,
+    // whose alpha (= opacity) is below 1/255, so those events never blend.
+    auto needs = [](float p, float thr_e) {
+        return !__builtin_islessgreater(__builtin_amdgcn_fmed3f(p, thr_e, 0.0f), p);
     };
     auto below = [](uint64_t m, uint32_t base0) {  // base0 + set bits of m below this lane
         return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
@@ -801,7 +785,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
-            const float thr = rl(d.thr, src);
+            const float thr = fminf(rl(d.thr, src), 0.0f);  // thr_e of needs()
             // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
             // pairs (x0, x1) and (y0, y1) in packed fp32 (v_pk_*): each element is the same
             // IEEE op sequence as the scalar formula
@@ -912,7 +896,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
-            const float thr = rl(d.thr, src);
+            const float thr = fminf(rl(d.thr, src), 0.0f);  // thr_e of needs()
             // :111-116, the same op sequence as the packed form below
             const float dx = sfx - mx, dy = sfy - my;
             const float p = -0.5f * ((ca * dx) * dx + (cc * dy) * dy) - (cbv * dx) * dy;

@@ -7,6 +7,9 @@
 //   k_upsweep    per 4096-key tile (8192 in pass 0), 256-bin digit histogram -> hist[digit][tile]
 //   k_scan_rows  one workgroup per digit: exclusive scan of hist[digit][*], row totals
 //   k_downsweep  wave64 ballot-match ranking (stable), LDS reorder, coalesced scatter
+// A frame's tile bins (countBins.glsl: a count per int(key), then its prefix) ride along: the
+// first upsweep also counts tiles, and one more workgroup of the last k_scan_rows launch
+// scans them (replacing two launches and a read of the keys).
 // Stability: inside a tile, wave w owns elements [w*1024, (w+1)*1024) in order and ranks them
 // sequentially (item k, then lane), so equal digits keep their input order; tiles are
 // ordered by the digit-major scan.  The result is therefore the unique stable sort -- the
@@ -28,6 +31,15 @@ constexpr int kRadix = 256;
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+constexpr int kTileCopies = 16;  // tile counters spread over copies (by workgroup): fewer same-address atomics
+
+// GLSL int(float) (countBins.glsl's int(key)): v_cvt_i32_f32 itself (truncate, saturate, NaN -> 0)
+__device__ __forceinline__ int f2i(float f) {
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
+}
 
 // mask of the active lanes whose 8-bit digit equals this lane's (8 ballots).  Per bit:
 // s = the lane's bit sign-extended, m &= ~(ballot ^ s) -- one v_bitop3 per mask half
@@ -82,17 +94,21 @@ __device__ __forceinline__ uint32_t elem_count(uint32_t n, const uint32_t *cnt) 
 
 // W waves per workgroup, tile = W * 1024 keys (the pass-0 sort uses W = 8: its random low
 // digits leave short runs per tile, so a larger tile doubles the scatter's write runs)
+// tile_counts != null: also countBins.glsl:20-31 -- tile_counts[int(key)] += 1 for int(key) in
+// [0, 256), LDS replicas, then one global atomic per nonzero tile and workgroup
 template <int W>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
-                                                    uint32_t *__restrict__ hist, uint32_t nb) {
+                                                    uint32_t *__restrict__ hist, uint32_t nb,
+                                                    uint32_t *__restrict__ tile_counts) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems;
     const uint32_t n = elem_count(n_max, cnt);
     if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count (never scanned)
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
-    for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) s_cnt[i] = 0;
+    __shared__ uint32_t s_tiles[kRadix * kRep];
+    for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) s_cnt[i] = s_tiles[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t base = blockIdx.x * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
@@ -112,23 +128,81 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
-        if (idx < n) atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
+        if (idx < n) {
+            atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
+            if (tile_counts) {  // uniform
+                const uint32_t t = (uint32_t)f2i(__uint_as_float(kk[k]));
+                if (t < (uint32_t)kRadix) atomicAdd(&s_tiles[t * kRep + rep], 1u);
+            }
+        }
     }
     __syncthreads();
     const int d = threadIdx.x;
     if (d >= kRadix) return;
-    const uint4 c0 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep]);
-    const uint4 c1 = *reinterpret_cast<const uint4 *>(&s_cnt[d * kRep + 4]);
-    hist[(size_t)d * nb + blockIdx.x] = (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
+    auto sum8 = [](const uint32_t *p) {
+        const uint4 c0 = *reinterpret_cast<const uint4 *>(p);
+        const uint4 c1 = *reinterpret_cast<const uint4 *>(p + 4);
+        return (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
+    };
+    hist[(size_t)d * nb + blockIdx.x] = sum8(&s_cnt[d * kRep]);
+    if (tile_counts) {
+        const uint32_t c = sum8(&s_tiles[d * kRep]);
+        if (c) atomicAdd(&tile_counts[(blockIdx.x % kTileCopies) * kRadix + d], c);
+    }
+}
+
+// tile bins from the tile counts (one workgroup of 1024): bins[t] = inclusive prefix, and the
+// draw's tile order bins[256 + r] = the tile with the r-th longest list (ties by index); the
+// counts are cleared for the next frame
+__device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w) {
+    __shared__ uint32_t s_c[kRadix];
+    __shared__ uint32_t s_part[4][kRadix];
+    const int t = threadIdx.x & (kRadix - 1), q = threadIdx.x >> 8;
+    if (q == 0) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < kTileCopies; ++k) {
+            c += counts[k * kRadix + t];
+            counts[k * kRadix + t] = 0;
+        }
+        s_c[t] = c;
+    }
+    __syncthreads();
+    const uint32_t v = s_c[t];
+    // rank = #tiles ahead of t: longer, or as long with a smaller index (4 quarters of u)
+    uint32_t r = 0;
+#pragma unroll 16
+    for (int u = 64 * q; u < 64 * q + 64; ++u) {
+        const uint32_t c = s_c[u];
+        r += (c > v || (c == v && u < t)) ? 1u : 0u;
+    }
+    s_part[q][t] = r;
+    // inclusive prefix of the counts over the first 4 waves
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(q == 0 ? v : 0u);
+    if (lane == 63 && wid < 4) s_w[wid] = inc;
+    __syncthreads();
+    if (q == 0) {
+        uint32_t off = 0;
+        for (int w = 0; w < wid; ++w) off += s_w[w];
+        bins[t] = off + inc;
+        bins[kRadix + s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t]] = (uint32_t)t;
+    }
 }
 
 // one block per digit: exclusive scan of that digit's per-tile counts (the tiles holding
-// elements; rows are nb long), row total
+// elements; rows are nb long), row total.  With bins != null, block 256 computes the tile
+// bins from tile_counts instead (bins_scan).
 __global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, uint32_t tile,
-                                                    uint32_t *__restrict__ row_total) {
+                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
+                                                    uint32_t *__restrict__ bins) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_carry;
+    if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
+        bins_scan(tile_counts, bins, s_w);
+        return;
+    }
     const uint32_t nb = (elem_count(n_max, cnt) + tile - 1) / tile;
     uint32_t *row = hist + (size_t)blockIdx.x * nb_stride;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
@@ -293,9 +367,12 @@ int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s) {
         }
         sc.hist_cap = cap;
     }
-    if (!sc.row_total && hipMalloc(&sc.row_total, kRadix * 4) != hipSuccess) {
-        err = "radix sort: out of device memory";
-        return GS_ERR_NOMEM;
+    if (!sc.row_total) {  // row totals [256] + tile counts [16][256] (zero between sorts)
+        const size_t bytes = (size_t)(1 + kTileCopies) * kRadix * 4;
+        if (hipMalloc(&sc.row_total, bytes) != hipSuccess || hipMemsetAsync(sc.row_total, 0, bytes, s) != hipSuccess) {
+            err = "radix sort: out of device memory";
+            return GS_ERR_NOMEM;
+        }
     }
     return GS_OK;
 }
@@ -309,8 +386,8 @@ void sort_free(SortScratch &sc) {
 }
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
-               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop) {
-    if ((n <= 1 && !dev_count) || n < 1) {  // nothing to sort; the timing events still mark the call
+               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins) {
+    if (((n <= 1 && !dev_count) || n < 1) && !bins) {  // nothing to sort; the events still mark the call
         if (start) (void)hipEventRecord(start, s);
         if (stop) (void)hipEventRecord(stop, s);
         return GS_OK;
@@ -319,8 +396,16 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         err = "radix sort: n must be < 2^31";
         return GS_ERR_INVALID;
     }
-    int rc = sort_ensure(sc, n, err, s);
+    int rc = sort_ensure(sc, std::max<int64_t>(n, 1), err, s);
     if (rc) return rc;
+    uint32_t *tile_counts = sc.row_total + kRadix;
+    if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
+        if (start) (void)hipEventRecord(start, s);
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + 1), dim3(1024), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
+                           tile_counts, bins);
+        if (stop) (void)hipEventRecord(stop, s);
+        return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
+    }
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
@@ -331,12 +416,13 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         if (big)
             hipExtLaunchKernelGGL(k_upsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin,
-                                  (uint32_t)n, dev_count, shift, sc.hist, nb);
+                                  (uint32_t)n, dev_count, shift, sc.hist, nb, bins ? tile_counts : nullptr);
         else
             hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
-                                  (uint32_t)n, dev_count, shift, sc.hist, nb);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n, dev_count, tile,
-                           sc.row_total);
+                                  (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
+        const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n,
+                           dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
         if (big)
             hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
                                   kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
