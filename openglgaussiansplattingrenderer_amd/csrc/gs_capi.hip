@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <thread>
 #include <vector>
@@ -917,6 +918,14 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     if (int rc = use_device(ctx)) return rc;
     const void *src = nullptr;
     size_t avail = 0, esz = 4;
+    // preprocess writes the blend records and boxes of splats with entries only; the rows of
+    // the others read as the values a culled splat gets (zeros, the empty box)
+    auto has_entries = [&](size_t rows, std::vector<int32_t> &ty) -> int {
+        ty.resize(rows);
+        GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->rec + 4, sizeof(int4), 4, rows,
+                                     hipMemcpyDeviceToHost, ctx->stream));
+        return GS_OK;
+    };
     switch (what) {
     case GS_READ_KEYS: src = ctx->keys; avail = (size_t)ctx->E; break;
     case GS_READ_VALS: src = ctx->vals; avail = (size_t)ctx->E; break;
@@ -930,14 +939,38 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         const size_t rows = (count + comps - 1) / comps;
         if (rows) {
             std::vector<float> tmp(rows * comps);
+            std::vector<int32_t> ty;
             GS_HIP(ctx, hipMemcpy2DAsync(tmp.data(), comps * 4, (const char *)ctx->sd + off, sizeof(gs::SplatDraw),
                                          comps * 4, rows, hipMemcpyDeviceToHost, ctx->stream));
+            if (int rc = has_entries(rows, ty)) return rc;
             GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            for (size_t r = 0; r < rows; ++r)
+                if (ty[r] < 0) std::fill(tmp.begin() + r * comps, tmp.begin() + (r + 1) * comps, 0.0f);
             std::memcpy(host_dst, tmp.data(), count * 4);
         }
         return GS_OK;
     }
-    case GS_READ_CULLBOX: src = ctx->cullbox; avail = 4 * (size_t)ctx->n; break;
+    case GS_READ_CULLBOX: {
+        if (count > 4 * (size_t)ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");
+        const size_t rows = (count + 3) / 4;
+        if (rows) {
+            std::vector<float> tmp(rows * 4);
+            std::vector<int32_t> ty;
+            GS_HIP(ctx, hipMemcpyAsync(tmp.data(), ctx->cullbox, rows * 16, hipMemcpyDeviceToHost, ctx->stream));
+            if (int rc = has_entries(rows, ty)) return rc;
+            GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            const float inf = std::numeric_limits<float>::infinity();
+            for (size_t r = 0; r < rows; ++r)
+                if (ty[r] < 0) {
+                    tmp[4 * r] = inf;
+                    tmp[4 * r + 1] = -inf;
+                    tmp[4 * r + 2] = inf;
+                    tmp[4 * r + 3] = -inf;
+                }
+            std::memcpy(host_dst, tmp.data(), count * 4);
+        }
+        return GS_OK;
+    }
     default: return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: unknown buffer");
     }
     if (count > avail) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");

@@ -253,10 +253,14 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
         // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
         // becomes -inf, which never skips
+        // the blend record, box and (GS_FLAG_SH) colour are read only through entries: written
+        // for the splats that have some (gs_frame_read shows the others as culled)
+        if (rc.y >= 0) {
         float thr = -logf(255.0f * co.w) - 1.0e-3f;
         if (thr != thr) thr = -__builtin_inff();
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
-        if (P.sh && rc.y >= 0) {  // GS_FLAG_SH: this frame's colour of a splat that has entries
+        fr.cullbox[i] = box;
+        if (P.sh) {  // GS_FLAG_SH: this frame's colour
             float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
             const float len = sqrtf(dx * dx + dy * dy + dz * dz);
             dx = dx / len;
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             fr.col[i] = make_float4(sh_channel(sc.sh, n, i, 0, dx, dy, dz), sh_channel(sc.sh, n, i, 1, dx, dy, dz),
                                     sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
         }
-        fr.cullbox[i] = box;
+        }
         fr.rec[i] = rc;
     }
     }

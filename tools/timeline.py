@@ -23,6 +23,8 @@ ctx.draw_stats(reset=True)
 sp.render_uniforms(u)
 st = ctx.draw_stats(reset=False)
 tr = ctx.draw_block_trace(65536).astype(np.int64)
+if len(sys.argv) > 3:  # save the raw trace and the bins (tile order) for offline analysis
+    np.savez(sys.argv[3], trace=tr, bins=sp.read(g.GS_READ_BINS, 256))
 live = tr[:, 1] != 0
 tr = tr[live]
 t0 = tr[:, 0].min()
