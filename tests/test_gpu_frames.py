@@ -104,3 +104,61 @@ def test_staged_calls_after_inflight_frames():
     img = sp.texture().reshape(-1)
     assert np.array_equal(img, out.download(np.uint8, W * H * 4))
     ctx.close()
+
+
+def near_camera_splats(ctx, W, H, n=20000, seed=5):
+    """splats scattered around the main camera: some land in front of the near plane, giving
+    negative keys (Q6) -- a key range far wider than 2^27 bit patterns"""
+    u = g.main_camera(W, H).uniforms()
+    V = np.array(u.view[:], np.float32).reshape(4, 4).T
+    campos = -V[:3, :3].T @ V[:3, 3]
+    rng = np.random.default_rng(seed)
+    means = (campos + rng.normal(size=(n, 3)) * 1.5).astype(np.float32)
+    rot = rng.normal(size=(n, 4)).astype(np.float32)
+    log_sc = rng.uniform(np.log(0.01), np.log(0.1), (n, 3)).astype(np.float32)
+    op = rng.normal(0, 2, n).astype(np.float32)
+    col = rng.normal(size=(n, 3)).astype(np.float32)
+    return g.Splats.from_raw(means, col, op, log_sc, rot, W, H, ctx=ctx)
+
+
+def test_wide_key_range_sorts_all_bits(oracle):
+    """a frame whose keys span more than 2^27 bit patterns sorts all 32 bits (4 passes); the
+    3-pass sort of narrow frames is exercised by every other frame test"""
+    W, H = 512, 384
+    ctx = g.Context(0)
+    sp = near_camera_splats(ctx, W, H)
+    u = g.main_camera(W, H).uniforms()
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    st = render_sync(sp, u, out)
+    E = int(st.entries)
+    keys = sp.read(g.GS_READ_KEYS, E)
+    vals = sp.read(g.GS_READ_VALS, E)
+    assert int(keys.max()) - int(keys.min()) >= 1 << 27, "the case must be wide"
+    ref = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0, draw=False)
+    assert np.array_equal(keys, ref["keys"]) and np.array_equal(vals, ref["vals"])
+    ctx.close()
+
+
+def test_wide_key_range_in_flight_renders_again():
+    """a frame enqueued without a round trip after narrow frames sorts in 3 passes; when its own
+    key range turns out wide it is detected at gs_sync and rendered again (4 passes)"""
+    W, H = 512, 384
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    narrow = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    wide = near_camera_splats(ctx, W, H)
+    u = g.main_camera(W, H).uniforms()
+    out_n = g.DeviceBuffer(ctx, W * H * 4)
+    out_w = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(narrow, u, out_n)  # narrow key range observed: the next frame sorts in 3 passes
+    render_spec(wide, u, out_w)
+    render_spec(narrow, u, out_n)  # a frame behind it, rendered again too
+    ctx.sync()
+    got_w = out_w.download(np.uint8, W * H * 4)
+    got_n = out_n.download(np.uint8, W * H * 4)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(wide, u, ref)
+    assert np.array_equal(got_w, ref.download(np.uint8, W * H * 4))
+    render_sync(narrow, u, ref)
+    assert np.array_equal(got_n, ref.download(np.uint8, W * H * 4))
+    ctx.close()
