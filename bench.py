@@ -2,7 +2,7 @@
 """bench.py -- frames/s at 1920x1080 on the bicycle-sized scene (+ radix-sort Gkeys/s), with
 the HBM roofline of the dominant kernel and a bounded CPU-oracle baseline.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2] [--clean] [--fast-exp]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c2] [--clean] [--fast-exp] [--lanes 1|2]
 
 One frame = one step of the hot path (preprocess -> sort -> bins -> blend) over the
 resident scene (BASELINE.json configs[2]: 6,131,954 splats at 1920x1080; the real bicycle
@@ -167,13 +167,16 @@ def load_pmc(kernel: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--clean", action="store_true", help="GS_FLAG_CLEAN: reference quirks fixed")
     ap.add_argument("--fast-exp", action="store_true", help="GS_FLAG_FAST_EXP: hardware exp in the blend")
     ap.add_argument("--sh", action="store_true", help="GS_FLAG_SH: degree-3 SH colours (SURVEY f3, beyond the "
                     "reference; seeded synthetic f_rest)")
+    ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
+                    help="frames in flight per GPU (gs_ctx_set_lanes): 2 overlaps frame k+1's preprocess / "
+                         "emission / sort with frame k's blend")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -187,6 +190,7 @@ def main():
     flags = ((g.GS_FLAG_CLEAN if args.clean else 0) | (g.GS_FLAG_FAST_EXP if args.fast_exp else 0) |
              (g.GS_FLAG_SH if args.sh else 0))
     ctx = g.Context(local)
+    ctx.set_lanes(args.lanes)
     sp, data_desc = load_scene(args.config, W, H, ctx, flags)
     if args.sh:
         rng = np.random.default_rng(4242)
@@ -212,12 +216,26 @@ def main():
     local_s = t1 - t0
     elapsed = max_over_ranks(pg, local_s)
     tm_draw = ctx.timing_read()
-    # per-stage breakdown: the same frames again with every stage boundary timed
+    # one frame at a time (gs_ctx_set_lanes 1): the frame latency, and the per-stage breakdown
+    # (the same frames again with every stage boundary timed, stages not sharing the GPU with
+    # the next frame's)
+    ctx.set_lanes(1)
+    for _ in range(2):
+        sp.render_uniforms(u)
+    ctx.sync()
+    ctx.timing_reset()
+    ts0 = time.perf_counter()
+    for _ in range(args.steps):
+        sp.render_uniforms(u)
+    ctx.sync()
+    serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
+    tm_serial = ctx.timing_read()
     ctx.timing_enable(g.GS_TIMING_STAGES)
     ctx.timing_reset()
     for _ in range(args.steps):
         sp.render_uniforms(u)
     tm = ctx.timing_read()
+    ctx.set_lanes(args.lanes)
     st = sp.stats
     N, V, D, E = int(st.num_splats), int(st.visible), int(st.duplicates), int(st.entries)
     frames_total = world * args.steps
@@ -247,8 +265,9 @@ def main():
     roofline = {"bound": "hbm", "kernel": kern_name, "stage": dom, "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(alg[dom]), "avg_launch_ms": round(stage_ms_dom, 4),
-                "avg_launch_ms_source": ("hipEvents on the draw dispatch over the timed frames" if dom == "draw"
-                                         else "hipEvents of the stage-timing pass"),
+                "avg_launch_ms_source": ("hipEvents on the draw dispatch over the timed frames" +
+                                         (" (sharing the GPU with the next frame's stages)" if args.lanes > 1 else "")
+                                         if dom == "draw" else "hipEvents of the stage-timing pass"),
                 "traffic": load_pmc(kern_name)}
     frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
     frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
@@ -279,10 +298,14 @@ def main():
                        (", fast exp" if args.fast_exp else ", defined exp") +
                        (", SH degree 3 (beyond the reference)" if args.sh else ""),
                        "splats": N, "width": W, "height": H, "views_per_gpu": 1,
-                       "parallelism": f"replicas x{world} (independent views, no collective)"},
+                       "parallelism": f"replicas x{world} (independent views, no collective); "
+                                      f"{args.lanes} frame(s) in flight per GPU"},
             "frame": {"V": V, "D": D, "E": E, "D_over_N": round(D / max(N, 1), 4),
                       "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-                      "stage_ms_source": "second pass of the same frames with every stage boundary timed",
+                      "stage_ms_source": "the same frames one at a time (1 lane) with every stage boundary timed",
+                      "frames_in_flight": args.lanes,
+                      "serial_ms_per_frame": round(serial_ms, 4),
+                      "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
                       "frame_hbm_frac_algorithmic": round(frame_frac, 4)},
             "roofline": roofline,
             "sort": sort,

@@ -90,7 +90,13 @@ const char *gs_last_error(const gs_ctx *ctx);
 int gs_ctx_create(int device, gs_ctx **out);
 void gs_ctx_destroy(gs_ctx *ctx);
 int gs_sync(gs_ctx *ctx);                    /* glFinish (src/Splats.cpp:595) */
-void *gs_stream(gs_ctx *ctx);                /* the ctx's hipStream_t, for interop */
+void *gs_stream(gs_ctx *ctx);                /* the hipStream_t of the newest frame, for interop
+                                                (after gs_sync no other ctx stream has work) */
+/* Frames in flight on the device: 2 (default) -- consecutive frames alternate between two
+ * streams with their own frame buffers, so frame k+1's preprocess, emission and sort overlap
+ * frame k's blend (blends stay in frame order; everything else behaves as one stream) -- or 1.
+ * Beyond the reference, whose gpuRender blocks per frame (src/Splats.cpp:580,595). */
+int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
 
 /* device memory helpers (callers without their own allocator, e.g. ctypes tests) */
 int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr);

@@ -108,6 +108,7 @@ SIGNATURES = {
     "gs_ctx_destroy": (None, [_vp]),
     "gs_sync": (_i, [_vp]),
     "gs_stream": (_vp, [_vp]),
+    "gs_ctx_set_lanes": (_i, [_vp, _i]),
     "gs_malloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
     "gs_free": (_i, [_vp, _vp]),
     "gs_memcpy_h2d": (_i, [_vp, _vp, _vp, _sz]),

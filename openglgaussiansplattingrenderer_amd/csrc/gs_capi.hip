@@ -21,11 +21,13 @@
 constexpr int kEv = 9;
 constexpr int kRing = 4;
 
-struct gs_ctx {
-    int device = 0;
+// A frame lane: a stream and the per-frame buffers of the frames it runs.  Consecutive frames
+// alternate between the ctx's lanes (two by default), so frame k+1's preprocess, emission and
+// sort run while frame k blends -- they fill the blend's tail and the gaps between kernels.
+// Frame k+1's blend waits for frame k's (outputs and the draw-stats buffer are written in frame
+// order); every other operation joins the lanes first (as if there were one stream).
+struct Lane {
     hipStream_t stream = nullptr;
-    std::string err;
-
     // per-splat frame buffers (sized by the largest scene rendered so far)
     int n_cap = 0;
     gs::SplatDraw *sd = nullptr;
@@ -42,13 +44,29 @@ struct gs_ctx {
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
     uint32_t *bins = nullptr;        // [256] tile ranges + [256] draw dispatch order
-    unsigned long long *draw_stats = nullptr;  // [8] GS_FLAG_DRAW_STATS counters
     // output staging (host-destination renders)
     uint32_t *img = nullptr;
     size_t img_cap = 0;
     // argsort key scratch
     uint32_t *ask = nullptr;
     size_t ask_cap = 0;
+    // ordering between lanes
+    hipEvent_t draw_done = nullptr;  // after this lane's newest blend
+    bool drew = false;
+    hipEvent_t aux_done = nullptr;   // after this lane's newest non-frame work
+    bool aux_pending = false;        // ... not yet waited for by the other lanes' frames
+    hipEvent_t tail = nullptr;       // scratch: "all work so far" on this lane
+};
+constexpr int kMaxLanes = 2;
+
+struct gs_ctx {
+    int device = 0;
+    std::string err;
+    Lane lane[kMaxLanes];
+    int nlanes = kMaxLanes;  // frames in flight on the device (gs_ctx_set_lanes)
+    int cur_lane = 0;
+    Lane *L = &lane[0];      // the lane of the newest frame (and of non-frame work)
+    unsigned long long *draw_stats = nullptr;  // GS_FLAG_DRAW_STATS trace (shared: blends are ordered)
     // frame state
     int stage = 0;  // 0 none, 1 preprocessed, 2 sorted, 3 binned
     int n = 0;
@@ -120,10 +138,49 @@ int use_device(gs_ctx *ctx) {
     return GS_OK;
 }
 
+// wait on the host for every lane
+int sync_lanes(gs_ctx *ctx) {
+    for (int i = 0; i < ctx->nlanes; ++i) GS_HIP(ctx, hipStreamSynchronize(ctx->lane[i].stream));
+    return GS_OK;
+}
+
+// non-frame work about to be enqueued on the current lane: order it after everything enqueued
+// so far on the other lanes (on the device), as a single stream would
+int join_lanes(gs_ctx *ctx) {
+    for (int i = 0; i < ctx->nlanes; ++i) {
+        Lane &o = ctx->lane[i];
+        if (&o == ctx->L) continue;
+        GS_HIP(ctx, hipEventRecord(o.tail, o.stream));
+        GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.tail, 0));
+    }
+    return GS_OK;
+}
+
+// ... and enqueued: the other lanes' next frames wait for it
+int mark_aux(gs_ctx *ctx) {
+    GS_HIP(ctx, hipEventRecord(ctx->L->aux_done, ctx->L->stream));
+    ctx->L->aux_pending = true;
+    return GS_OK;
+}
+
+// a new frame starts: move to the next lane; it waits (on the device) for non-frame work
+// enqueued on the other lanes since their last frame
+int next_lane(gs_ctx *ctx) {
+    ctx->cur_lane = (ctx->cur_lane + 1) % ctx->nlanes;
+    ctx->L = &ctx->lane[ctx->cur_lane];
+    for (int i = 0; i < ctx->nlanes; ++i) {
+        Lane &o = ctx->lane[i];
+        if (&o == ctx->L || !o.aux_pending) continue;
+        GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.aux_done, 0));
+        o.aux_pending = false;
+    }
+    return GS_OK;
+}
+
 template <typename T>
 int grow(gs_ctx *ctx, T *&p, size_t count) {
     if (p) {  // frames in flight may still use the old buffer
-        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
         (void)hipFree(p);
     }
     p = nullptr;
@@ -132,35 +189,35 @@ int grow(gs_ctx *ctx, T *&p, size_t count) {
 }
 
 int ensure_splats(gs_ctx *ctx, int n) {
-    if (n <= ctx->n_cap) return GS_OK;
+    if (n <= ctx->L->n_cap) return GS_OK;
     const int cap = n;
     const int nb = gs::preprocess_blocks(cap);
     int rc;
-    if ((rc = grow(ctx, ctx->sd, cap)) || (rc = grow(ctx, ctx->cullbox, cap)) ||
-        (rc = grow(ctx, ctx->rec, cap)) || (rc = grow(ctx, ctx->blocksum, nb)))
+    if ((rc = grow(ctx, ctx->L->sd, cap)) || (rc = grow(ctx, ctx->L->cullbox, cap)) ||
+        (rc = grow(ctx, ctx->L->rec, cap)) || (rc = grow(ctx, ctx->L->blocksum, nb)))
         return rc;
-    ctx->n_cap = cap;
+    ctx->L->n_cap = cap;
     return GS_OK;
 }
 
 int ensure_entries(gs_ctx *ctx, int64_t e) {
-    if (e <= ctx->e_cap) return GS_OK;
+    if (e <= ctx->L->e_cap) return GS_OK;
     const int64_t cap = e + e / 4 + 4096;
     int rc;
-    if ((rc = grow(ctx, ctx->keys, (size_t)cap)) || (rc = grow(ctx, ctx->vals, (size_t)cap))) return rc;
-    ctx->e_cap = cap;
+    if ((rc = grow(ctx, ctx->L->keys, (size_t)cap)) || (rc = grow(ctx, ctx->L->vals, (size_t)cap))) return rc;
+    ctx->L->e_cap = cap;
     return GS_OK;
 }
 
 gs::FrameDev frame_dev(gs_ctx *ctx) {
     gs::FrameDev f;
-    f.sd = ctx->sd;
-    f.cullbox = ctx->cullbox;
-    f.rec = ctx->rec;
-    f.blocksum = ctx->blocksum;
-    f.totals = ctx->totals;
+    f.sd = ctx->L->sd;
+    f.cullbox = ctx->L->cullbox;
+    f.rec = ctx->L->rec;
+    f.blocksum = ctx->L->blocksum;
+    f.totals = ctx->L->totals;
     f.h_totals = ctx->h_ring_dev + 4 * ctx->cur;
-    f.col = ctx->col;
+    f.col = ctx->L->col;
     return f;
 }
 
@@ -221,7 +278,7 @@ int oldest_used(const gs_ctx *ctx, uint64_t seq_limit) {
 // ones are the newest (every host-synchronous operation validates first), so grow the entry
 // buffers and render them again, in order, through the synchronous path.
 int handle_overflow(gs_ctx *ctx) {
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_lanes(ctx)) return rc;
     gs_ctx::Slot redo[kRing];
     int nredo = 0;
     int64_t need = 0;
@@ -269,7 +326,7 @@ bool any_spec(const gs_ctx *ctx) {
 // are on the host)
 int validate_all(gs_ctx *ctx) {
     if (!any_spec(ctx)) return GS_OK;
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_lanes(ctx)) return rc;
     return retire_upto(ctx, ~0ull);
 }
 
@@ -319,15 +376,23 @@ int gs_ctx_create(int device, gs_ctx **out) {
         return code;
     };
     if ((rc = use_device(ctx))) return fail(rc);
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess)
-        return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate failed"));
-    if (hipMalloc(&ctx->totals, 16) != hipSuccess || hipHostMalloc(&ctx->h_ring, 16 * kRing, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc(&ctx->bin_counts, 256 * 4) != hipSuccess || hipMalloc(&ctx->bins, 512 * 4) != hipSuccess ||
+    for (Lane &ln : ctx->lane) {
+        if (hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ln.draw_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ln.aux_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ln.tail, hipEventDisableTiming) != hipSuccess)
+            return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
+        if (hipMalloc(&ln.totals, 16) != hipSuccess || hipMalloc(&ln.bin_counts, 256 * 4) != hipSuccess ||
+            hipMalloc(&ln.bins, 512 * 4) != hipSuccess)
+            return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
+        if (hipMemset(ln.bin_counts, 0, 256 * 4) != hipSuccess)
+            return fail(set_error(nullptr, GS_ERR_HIP, "ctx setup failed"));
+    }
+    if (hipHostMalloc(&ctx->h_ring, 16 * kRing, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&ctx->draw_stats, gs::kDrawStatsBytes) != hipSuccess ||
         hipMemset(ctx->draw_stats, 0, gs::kDrawStatsBytes) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
-    if (hipHostGetDevicePointer((void **)&ctx->h_ring_dev, ctx->h_ring, 0) != hipSuccess ||
-        hipMemset(ctx->bin_counts, 0, 256 * 4) != hipSuccess)
+    if (hipHostGetDevicePointer((void **)&ctx->h_ring_dev, ctx->h_ring, 0) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_HIP, "ctx setup failed"));
     // stage events are timing-only: no system-scope fence (its cache writeback / invalidate
     // idles the stream for microseconds); the frame-end event keeps it, since the host reads
@@ -347,30 +412,48 @@ int gs_ctx_create(int device, gs_ctx **out) {
 void gs_ctx_destroy(gs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (Lane &ln : ctx->lane)
+        if (ln.stream) (void)hipStreamSynchronize(ln.stream);
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
-    void *bufs[] = {ctx->sd, ctx->cullbox, ctx->rec, ctx->blocksum, ctx->totals, ctx->keys, ctx->vals,
-                    ctx->bin_counts, ctx->bins, ctx->img, ctx->ask, ctx->draw_stats, ctx->col};
-    for (void *b : bufs)
-        if (b) (void)hipFree(b);
+    for (Lane &ln : ctx->lane) {
+        void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals,
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col};
+        for (void *b : bufs)
+            if (b) (void)hipFree(b);
+        gs::sort_free(ln.sort);
+        for (hipEvent_t e : {ln.draw_done, ln.aux_done, ln.tail})
+            if (e) (void)hipEventDestroy(e);
+        if (ln.stream) (void)hipStreamDestroy(ln.stream);
+    }
+    if (ctx->draw_stats) (void)hipFree(ctx->draw_stats);
     if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
-    gs::sort_free(ctx->sort);
     for (auto &set : ctx->ev)
         for (auto &e : set)
             if (e) (void)hipEventDestroy(e);
     for (auto &e : ctx->evs)
         if (e) (void)hipEventDestroy(e);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+// frames in flight on the device: 2 (default: frame k+1's preprocess / emission / sort overlap
+// frame k's blend) or 1 (frames run one after the other on one stream)
+int gs_ctx_set_lanes(gs_ctx *ctx, int lanes) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (lanes < 1 || lanes > kMaxLanes) return set_error(ctx, GS_ERR_INVALID, "gs_ctx_set_lanes: lanes must be 1 or 2");
+    if (int rc = gs_sync(ctx)) return rc;
+    ctx->nlanes = lanes;
+    ctx->cur_lane = std::min(ctx->cur_lane, lanes - 1);
+    ctx->L = &ctx->lane[ctx->cur_lane];
+    return GS_OK;
 }
 
 int gs_sync(gs_ctx *ctx) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (Lane &ln : ctx->lane) GS_HIP(ctx, hipStreamSynchronize(ln.stream));
     return validate_all(ctx);  // speculative frames checked (and rendered again if they overflowed)
 }
 
-void *gs_stream(gs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+void *gs_stream(gs_ctx *ctx) { return ctx ? (void *)ctx->L->stream : nullptr; }
 
 int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr) {
     if (!ctx || !dptr) return set_error(ctx, GS_ERR_INVALID, "null argument");
@@ -387,21 +470,23 @@ int gs_free(gs_ctx *ctx, void *dptr) {
 }
 int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = join_lanes(ctx)) return rc;  // frames in flight may read dst
+    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     return GS_OK;
 }
 int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (int rc = gs_sync(ctx)) return rc;  // speculative frames complete and checked first
-    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     return GS_OK;
 }
 int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    GS_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream));
-    return GS_OK;
+    if (int rc = join_lanes(ctx)) return rc;
+    GS_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->L->stream));
+    return mark_aux(ctx);
 }
 
 // ------------------------------------------------------------------ host side
@@ -477,9 +562,9 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
         gs_scene_destroy(s);
         return set_error(ctx, GS_ERR_NOMEM, "gs_scene_create: out of device memory");
     }
-    GS_HIP(ctx, hipMemcpyAsync(s->soa, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    if (n > 0) GS_HIP(ctx, hipMemcpyAsync(s->colour, colours4, nn * sizeof(float4), hipMemcpyHostToDevice, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GS_HIP(ctx, hipMemcpyAsync(s->soa, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, ctx->L->stream));
+    if (n > 0) GS_HIP(ctx, hipMemcpyAsync(s->colour, colours4, nn * sizeof(float4), hipMemcpyHostToDevice, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     ctx->scenes.push_back(s);
     *out = s;
     return GS_OK;
@@ -534,7 +619,7 @@ int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out) {
     float *h_buf[2] = {nullptr, nullptr}, *d_buf[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
     auto cleanup = [&](int rc, const std::string &msg) {
-        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->L->stream);
         for (int k = 0; k < 2; ++k) {
             if (h_buf[k]) (void)hipHostFree(h_buf[k]);
             if (d_buf[k]) (void)hipFree(d_buf[k]);
@@ -562,10 +647,10 @@ int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out) {
             return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipEventSynchronize failed");
         if (!read_records(f, (char *)h_buf[k], cnt * rec))  // src/Splats.cpp:333-340
             return cleanup(GS_ERR_IO, "Error: failed to read all splats from file");
-        if (hipMemcpyAsync(d_buf[k], h_buf[k], cnt * rec, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+        if (hipMemcpyAsync(d_buf[k], h_buf[k], cnt * rec, hipMemcpyHostToDevice, ctx->L->stream) != hipSuccess)
             return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipMemcpyAsync failed");
-        gs::launch_ply_activate(ctx->stream, d_buf[k], (int)cnt, (int)base, n, s->soa, s->colour);
-        if (hipEventRecord(done[k], ctx->stream) != hipSuccess)
+        gs::launch_ply_activate(ctx->L->stream, d_buf[k], (int)cnt, (int)base, n, s->soa, s->colour);
+        if (hipEventRecord(done[k], ctx->L->stream) != hipSuccess)
             return cleanup(GS_ERR_HIP, "gs_scene_load_ply: hipEventRecord failed");
     }
     if (std::fgetc(f) != EOF) return cleanup(GS_ERR_IO, "Error: failed to read all splats from file");
@@ -583,10 +668,10 @@ int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *
     if (int rc = use_device(ctx)) return rc;
     const size_t nn = (size_t)scene->n;
     std::vector<float> soa(10 * nn);
-    if (nn) GS_HIP(ctx, hipMemcpyAsync(soa.data(), scene->soa, soa.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (nn) GS_HIP(ctx, hipMemcpyAsync(soa.data(), scene->soa, soa.size() * 4, hipMemcpyDeviceToHost, ctx->L->stream));
     if (nn && colours4)
-        GS_HIP(ctx, hipMemcpyAsync(colours4, scene->colour, nn * sizeof(float4), hipMemcpyDeviceToHost, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        GS_HIP(ctx, hipMemcpyAsync(colours4, scene->colour, nn * sizeof(float4), hipMemcpyDeviceToHost, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     for (size_t i = 0; i < nn; ++i) {
         if (means4) {
             means4[4 * i + 0] = soa[i];
@@ -616,8 +701,8 @@ int gs_scene_set_sh(gs_scene *scene, const float *f_dc3, const float *f_rest45) 
         }
     if (!scene->sh && hipMalloc(&scene->sh, planes.size() * 4) != hipSuccess)
         return set_error(ctx, GS_ERR_NOMEM, "gs_scene_set_sh: out of device memory");
-    GS_HIP(ctx, hipMemcpyAsync(scene->sh, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GS_HIP(ctx, hipMemcpyAsync(scene->sh, planes.data(), planes.size() * 4, hipMemcpyHostToDevice, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     return GS_OK;
 }
 
@@ -670,15 +755,15 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
     return use_device(ctx);
 }
 
-// preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->totals
+// preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->L->totals
 int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {
     const int n = scene->n;
     const bool sh = (flags & GS_FLAG_SH) != 0;
     if (sh && !scene->sh) return set_error(ctx, GS_ERR_INVALID, "GS_FLAG_SH: the scene has no SH (gs_scene_set_sh)");
     if (int rc = ensure_splats(ctx, n)) return rc;
-    if (sh && ctx->col_cap < n) {
-        if (int rc = grow(ctx, ctx->col, (size_t)n)) return rc;
-        ctx->col_cap = n;
+    if (sh && ctx->L->col_cap < n) {
+        if (int rc = grow(ctx, ctx->L->col, (size_t)n)) return rc;
+        ctx->L->col_cap = n;
     }
     if (int rc = begin_frame(ctx)) return rc;
     ctx->flags = flags;
@@ -690,16 +775,16 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
                         u->view[4 * c + 2] * u->view[14]);
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = gs::preprocess_blocks(n);
-    // k_scan_blocksums writes (V, D) to ctx->totals and to this slot's pinned host copy
-    gs::launch_preprocess(ctx->stream, P, scene_dev(scene), fr, fev(ctx, 0));
-    gs::launch_scan_blocksums(ctx->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
+    // k_scan_blocksums writes (V, D) to ctx->L->totals and to this slot's pinned host copy
+    gs::launch_preprocess(ctx->L->stream, P, scene_dev(scene), fr, fev(ctx, 0));
+    gs::launch_scan_blocksums(ctx->L->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
     return GS_OK;
 }
 
 int enqueue_emit(gs_ctx *ctx) {
-    gs::launch_emit(ctx->stream, ctx->n, frame_dev(ctx), ctx->keys, ctx->vals, (uint32_t)ctx->e_cap, fev(ctx, 2),
+    gs::launch_emit(ctx->L->stream, ctx->n, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
                     fev(ctx, 3));
     GS_HIP(ctx, hipGetLastError());
     return GS_OK;
@@ -709,16 +794,16 @@ int enqueue_emit(gs_ctx *ctx) {
 // with_bins: the tile bins (gs_compute_bins' output) come from the sort's own histogram read;
 // the bins stage is then empty (its timing event follows the sort's)
 int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false) {
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->keys, ctx->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5), with_bins ? ctx->bins : nullptr))
+    if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
+                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr))
         return set_error(ctx, rc, ctx->err);
     if (with_bins)
-        if (hipEvent_t e = fev(ctx, 6)) GS_HIP(ctx, hipEventRecord(e, ctx->stream));
+        if (hipEvent_t e = fev(ctx, 6)) GS_HIP(ctx, hipEventRecord(e, ctx->L->stream));
     return GS_OK;
 }
 
 int enqueue_bins(gs_ctx *ctx, int64_t E, const uint32_t *count) {
-    gs::launch_bins(ctx->stream, ctx->keys, E, count, ctx->bin_counts, ctx->bins, fev(ctx, 6));
+    gs::launch_bins(ctx->L->stream, ctx->L->keys, E, count, ctx->L->bin_counts, ctx->L->bins, fev(ctx, 6));
     GS_HIP(ctx, hipGetLastError());
     return GS_OK;
 }
@@ -760,22 +845,29 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     const size_t npx = (size_t)width * height;
     uint32_t *dst = (uint32_t *)out_rgba8;
     if (!out_on_device) {
-        if (npx > ctx->img_cap) {
-            if (int rc = grow(ctx, ctx->img, npx)) return rc;
-            ctx->img_cap = npx;
+        if (npx > ctx->L->img_cap) {
+            if (int rc = grow(ctx, ctx->L->img, npx)) return rc;
+            ctx->L->img_cap = npx;
         }
-        dst = ctx->img;
+        dst = ctx->L->img;
     }
     P.coverW = coverW;
     P.coverH = coverH;
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
-    const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->col : scene->colour;
-    gs::launch_draw(ctx->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->bins, ctx->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
+    const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
+    // blends run in frame order: wait for the other lanes' newest blend
+    for (int i = 0; i < ctx->nlanes; ++i) {
+        Lane &o = ctx->lane[i];
+        if (&o != ctx->L && o.drew) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.draw_done, 0));
+    }
+    gs::launch_draw(ctx->L->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->L->bins, ctx->L->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
                     fev(ctx, 8));
     GS_HIP(ctx, hipGetLastError());
+    GS_HIP(ctx, hipEventRecord(ctx->L->draw_done, ctx->L->stream));
+    ctx->L->drew = true;
     if (!out_on_device) {
-        GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
-        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->L->stream));
+        GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     }
     return GS_OK;
 }
@@ -796,8 +888,9 @@ int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
 // the device and are sized by the entry capacity (last observed count + 25 % + 64Ki); the
 // slot keeps what is needed to render the frame again should the count exceed it.
 int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out) {
+    if (int rc = next_lane(ctx)) return rc;
     const int64_t want = std::max<int64_t>(ctx->E + ctx->E / 4 + 65536, (int64_t)scene->n + 4096);
-    if (ctx->e_cap < want)
+    if (ctx->L->e_cap < want)
         if (int rc = ensure_entries(ctx, want)) return rc;
     if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
     gs_ctx::Slot &sl = ctx->slot[ctx->cur];
@@ -806,13 +899,13 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     sl.u = *u;
     sl.flags = flags;
     sl.out = out;
-    sl.cap = ctx->e_cap;
-    const uint32_t *cnt = ctx->totals;
+    sl.cap = ctx->L->e_cap;
+    const uint32_t *cnt = ctx->L->totals;
     int rc;
-    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->e_cap, cnt, true)))
+    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true)))
         return rc;
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
-                           out, 1, ctx->e_cap, cnt)))
+                           out, 1, ctx->L->e_cap, cnt)))
         return rc;
     ctx->stage = 3;
     return GS_OK;
@@ -825,10 +918,11 @@ extern "C" {
 int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, gs_frame_stats *stats) {
     if (int rc = check_frame_args(ctx, scene, u, "gs_preprocess")) return rc;
     if (int rc = validate_all(ctx)) return rc;
+    if (int rc = next_lane(ctx)) return rc;  // a new frame
     if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
     // E is needed on the host to size the sort (the reference maps its atomic counter back
     // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));  // (V, D) are in the slot's pinned copy
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));  // (V, D) are in the slot's pinned copy
     ctx->V = ctx->h_ring[4 * ctx->cur];
     ctx->D = ctx->h_ring[4 * ctx->cur + 1];
     ctx->E = ctx->V + ctx->D;
@@ -922,16 +1016,16 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     // the others read as the values a culled splat gets (zeros, the empty box)
     auto has_entries = [&](size_t rows, std::vector<int32_t> &ty) -> int {
         ty.resize(rows);
-        GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->rec + 4, sizeof(int4), 4, rows,
-                                     hipMemcpyDeviceToHost, ctx->stream));
+        GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->L->rec + 4, sizeof(int4), 4, rows,
+                                     hipMemcpyDeviceToHost, ctx->L->stream));
         return GS_OK;
     };
     switch (what) {
-    case GS_READ_KEYS: src = ctx->keys; avail = (size_t)ctx->E; break;
-    case GS_READ_VALS: src = ctx->vals; avail = (size_t)ctx->E; break;
+    case GS_READ_KEYS: src = ctx->L->keys; avail = (size_t)ctx->E; break;
+    case GS_READ_VALS: src = ctx->L->vals; avail = (size_t)ctx->E; break;
     case GS_READ_BINS:
         if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");
-        src = ctx->bins; avail = 256; break;
+        src = ctx->L->bins; avail = 256; break;
     case GS_READ_MEANS2D:
     case GS_READ_CONICS: {  // fields of the 32-byte blend records
         const size_t comps = what == GS_READ_MEANS2D ? 2 : 4, off = what == GS_READ_MEANS2D ? 0 : 8;
@@ -940,10 +1034,10 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         if (rows) {
             std::vector<float> tmp(rows * comps);
             std::vector<int32_t> ty;
-            GS_HIP(ctx, hipMemcpy2DAsync(tmp.data(), comps * 4, (const char *)ctx->sd + off, sizeof(gs::SplatDraw),
-                                         comps * 4, rows, hipMemcpyDeviceToHost, ctx->stream));
+            GS_HIP(ctx, hipMemcpy2DAsync(tmp.data(), comps * 4, (const char *)ctx->L->sd + off, sizeof(gs::SplatDraw),
+                                         comps * 4, rows, hipMemcpyDeviceToHost, ctx->L->stream));
             if (int rc = has_entries(rows, ty)) return rc;
-            GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
             for (size_t r = 0; r < rows; ++r)
                 if (ty[r] < 0) std::fill(tmp.begin() + r * comps, tmp.begin() + (r + 1) * comps, 0.0f);
             std::memcpy(host_dst, tmp.data(), count * 4);
@@ -956,9 +1050,9 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         if (rows) {
             std::vector<float> tmp(rows * 4);
             std::vector<int32_t> ty;
-            GS_HIP(ctx, hipMemcpyAsync(tmp.data(), ctx->cullbox, rows * 16, hipMemcpyDeviceToHost, ctx->stream));
+            GS_HIP(ctx, hipMemcpyAsync(tmp.data(), ctx->L->cullbox, rows * 16, hipMemcpyDeviceToHost, ctx->L->stream));
             if (int rc = has_entries(rows, ty)) return rc;
-            GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
             const float inf = std::numeric_limits<float>::infinity();
             for (size_t r = 0; r < rows; ++r)
                 if (ty[r] < 0) {
@@ -975,8 +1069,8 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     }
     if (count > avail) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");
     if (count) {
-        GS_HIP(ctx, hipMemcpyAsync(host_dst, src, count * esz, hipMemcpyDeviceToHost, ctx->stream));
-        GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        GS_HIP(ctx, hipMemcpyAsync(host_dst, src, count * esz, hipMemcpyDeviceToHost, ctx->L->stream));
+        GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     }
     return GS_OK;
 }
@@ -986,23 +1080,25 @@ int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n
     if (!ctx || (n > 0 && (!d_keys || !d_order)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_argsort_f32: bad argument");
     if (n <= 1) return GS_OK;
     if (int rc = use_device(ctx)) return rc;
-    if ((size_t)n > ctx->ask_cap) {
-        if (int rc = grow(ctx, ctx->ask, (size_t)n + (size_t)n / 4)) return rc;
-        ctx->ask_cap = (size_t)n + (size_t)n / 4;
+    if ((size_t)n > ctx->L->ask_cap) {
+        if (int rc = grow(ctx, ctx->L->ask, (size_t)n + (size_t)n / 4)) return rc;
+        ctx->L->ask_cap = (size_t)n + (size_t)n / 4;
     }
-    gs::launch_gather_keys(ctx->stream, d_keys, d_order, ctx->ask, n, ctx->evs[0]);
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, ctx->ask, (uint32_t *)d_order, n, ctx->err, nullptr, nullptr,
+    if (int rc = join_lanes(ctx)) return rc;
+    gs::launch_gather_keys(ctx->L->stream, d_keys, d_order, ctx->L->ask, n, ctx->evs[0]);
+    if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->ask, (uint32_t *)d_order, n, ctx->err, nullptr, nullptr,
                                 ctx->evs[1]))
         return set_error(ctx, rc, ctx->err);
-    return GS_OK;
+    return mark_aux(ctx);
 }
 
 int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n) {
     if (!ctx || (n > 0 && (!d_keys || !d_vals)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_sort_pairs_u32: bad argument");
     if (int rc = use_device(ctx)) return rc;
-    if (int rc = gs::sort_pairs(ctx->stream, ctx->sort, d_keys, d_vals, n, ctx->err, nullptr, ctx->evs[0], ctx->evs[1]))
+    if (int rc = join_lanes(ctx)) return rc;
+    if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, d_keys, d_vals, n, ctx->err, nullptr, ctx->evs[0], ctx->evs[1]))
         return set_error(ctx, rc, ctx->err);
-    return GS_OK;
+    return mark_aux(ctx);
 }
 
 int gs_last_kernel_ms(gs_ctx *ctx, int kernel, float *ms) {
@@ -1018,9 +1114,9 @@ int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset) {
     if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "null argument");
     if (int rc = gs_sync(ctx)) return rc;
     std::vector<uint32_t> tr((size_t)gs::kDrawTraceBlocks * gs::kDrawTraceWords);
-    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-    if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, gs::kDrawStatsBytes, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->L->stream));
+    if (reset) GS_HIP(ctx, hipMemsetAsync(ctx->draw_stats, 0, gs::kDrawStatsBytes, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     std::memset(out, 0, 16 * sizeof(uint64_t));
     for (int b = 0; b < gs::kDrawTraceBlocks; ++b) {
         const uint32_t *r = tr.data() + (size_t)b * gs::kDrawTraceWords;
@@ -1046,8 +1142,8 @@ int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks) {
     if (int rc = gs_sync(ctx)) return rc;
     const int n = std::min(max_blocks, gs::kDrawTraceBlocks);
     std::vector<uint32_t> tr((size_t)n * gs::kDrawTraceWords);
-    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-    GS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    GS_HIP(ctx, hipMemcpyAsync(tr.data(), ctx->draw_stats, tr.size() * 4, hipMemcpyDeviceToHost, ctx->L->stream));
+    GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
     std::memcpy(out, tr.data(), tr.size() * 4);
     return n;
 }

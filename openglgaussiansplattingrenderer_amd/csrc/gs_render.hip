@@ -549,15 +549,17 @@ __device__ __forceinline__ uint32_t pack_rgba8(const float4 &c) {
 // minimise the 1-D quadratic along each edge (clamped).  The splat is dropped only when that
 // minimum exceeds the threshold by margins far above the rounding of power (relative error
 // <= ~6 eps * cond; conics with cond >= 1e4 are never dropped here).
+// Branch-free (every lane evaluates every term; the tests select): early returns here became
+// nested exec-mask branches costing more scalar instructions than the arithmetic they skipped.
 __device__ __forceinline__ bool ellipse_misses_rect(float mx, float my, float a, float b, float c, float thr,
                                                     float x0, float x1, float y0, float y1) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     const float lim = -2.0f * thr;  // pixels with q <= lim may blend
-    if (!(lim > 0.0f)) return thr > 0.0f;  // thr > 0: no power <= 0 reaches it; NaN / 0: keep
     const float det = a * c - b * b, tr = a + c;
-    if (!(a > 0.0f && c > 0.0f && det > 0.0f && tr * tr < 1.0e4f * det)) return false;
+    // well conditioned (else never dropped)
+    const bool ok = (a > 0.0f) & (c > 0.0f) & (det > 0.0f) & (tr * tr < 1.0e4f * det);
     const f2 X = f2{x0, x1} - f2{mx, mx}, Y = f2{y0, y1} - f2{my, my};
-    if (X.x <= 0.0f && X.y >= 0.0f && Y.x <= 0.0f && Y.y >= 0.0f) return false;  // centre inside
+    const bool inside = (X.x <= 0.0f) & (X.y >= 0.0f) & (Y.x <= 0.0f) & (Y.y >= 0.0f);  // centre inside: keep
     // edge minimisers via v_rcp (1 ulp): a minimiser off by delta raises q by O(delta^2),
     // orders of magnitude inside the margins below; both edges of a pair in packed fp32
     const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
@@ -571,7 +573,9 @@ __device__ __forceinline__ bool ellipse_misses_rect(float mx, float my, float a,
     dx = __builtin_elementwise_min(__builtin_elementwise_max(dx, f2{X.x, X.x}), f2{X.y, X.y});
     const f2 qy = A * dx * dx + two * B * dx * Y + C * Y * Y;
     const float qmin = fminf(fminf(qx.x, qx.y), fminf(qy.x, qy.y));
-    return qmin > lim * 1.002f + 1.0e-3f;
+    const bool far = ok & !inside & (qmin > lim * 1.002f + 1.0e-3f);  // (NaN: kept)
+    // lim <= 0 or NaN: thr > 0 means no power <= 0 reaches alpha 1/255 (dropped); NaN / 0: kept
+    return (lim > 0.0f) ? far : (thr > 0.0f);
 }
 
 // order this wave's LDS writes before its later LDS reads (single-wave workgroup)
@@ -683,11 +687,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         return o;
     };
     // does a pixel of power p need the exp / blend path?  :118-126 continue on p > 0, plus the
-    // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr_e, 0) == p or unordered (one
-    // compare), thr_e = min(thr, 0).  For thr > 0 (opacity < ~1/255) it admits p = +-0 only,
-    // whose alpha (= opacity) is below 1/255, so those events never blend.
-    auto needs = [](float p, float thr_e) {
-        return !__builtin_islessgreater(__builtin_amdgcn_fmed3f(p, thr_e, 0.0f), p);
+    // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr, 0) == p or unordered (one
+    // compare).  For thr > 0 (opacity < ~1/255) it admits p in [0, thr] instead, where
+    // exp(p) * o <= e^-0.001 / 255 < 1/255 (thr = -ln(255 o) - 1e-3, margins far above the
+    // rounding): those events never blend, as draw.glsl skips them.
+    auto needs = [](float p, float thr) {
+        return !__builtin_islessgreater(__builtin_amdgcn_fmed3f(p, thr, 0.0f), p);
     };
     auto below = [](uint64_t m, uint32_t base0) {  // base0 + set bits of m below this lane
         return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, base0));
@@ -781,15 +786,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // survivors left for the sparse phase).
     auto blend_dense = [&](uint64_t &keep, const SurvData &d, const SurvRgb &c) {
         // exact cull of the survivors (uniform keep mask)
-        if (cull) keep &= ~ballot(((keep >> lane) & 1ull) &&
-                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
+        if (cull && keep)  // uniform
+            keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         while (keep && !all_done) {
             const int src = __builtin_ctzll(keep);
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
-            const float thr = fminf(rl(d.thr, src), 0.0f);  // thr_e of needs()
+            const float thr = rl(d.thr, src);
             // :111-116, per pixel: -0.5*((a*dx)*dx + (c*dy)*dy) - (b*dx)*dy
             // pairs (x0, x1) and (y0, y1) in packed fp32 (v_pk_*): each element is the same
             // IEEE op sequence as the scalar formula
@@ -888,8 +893,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 
     // sparse phase (see go_sparse): one pixel per lane, state in registers
     auto blend_sparse = [&](uint64_t keep, const SurvData &d, const SurvRgb &c) {
-        if (cull) keep &= ~ballot(((keep >> lane) & 1ull) &&
-                                  ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
+        if (cull && keep)  // uniform
+            keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         if (!keep) return;  // uniform
         float4 pc = s_col[spix];
@@ -900,7 +905,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
-            const float thr = fminf(rl(d.thr, src), 0.0f);  // thr_e of needs()
+            const float thr = rl(d.thr, src);
             // :111-116, the same op sequence as the packed form below
             const float dx = sfx - mx, dy = sfy - my;
             const float p = -0.5f * ((ca * dx) * dx + (cc * dy) * dy) - (cbv * dx) * dy;

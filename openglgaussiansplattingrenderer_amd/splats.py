@@ -47,6 +47,11 @@ class Context:
     def sync(self):
         check(lib().gs_sync(self.handle), self.handle)
 
+    def set_lanes(self, lanes: int):
+        """frames in flight on the device (gs_ctx_set_lanes): 2 (default) overlaps frame k+1's
+        preprocess / emission / sort with frame k's blend; 1 runs frames one after the other"""
+        check(lib().gs_ctx_set_lanes(self.handle, int(lanes)), self.handle)
+
     def timing_reset(self):
         check(lib().gs_timing_reset(self.handle), self.handle)
 

@@ -162,3 +162,59 @@ def test_wide_key_range_in_flight_renders_again():
     render_sync(narrow, u, ref)
     assert np.array_equal(got_n, ref.download(np.uint8, W * H * 4))
     ctx.close()
+
+
+def test_two_lanes_keep_frame_order():
+    """consecutive frames alternate between two lanes (streams); blends into one output land in
+    frame order, and non-frame work between frames is ordered as on one stream"""
+    W, H = 384, 256
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, pose(W, H, 6), ref)
+    want_last = ref.download(np.uint8, W * H * 4)
+    render_sync(sp, pose(W, H, 0), out)
+    for k in range(7):  # the last frame written must be pose 6's
+        render_spec(sp, pose(W, H, k), out)
+    ctx.sync()
+    assert np.array_equal(out.download(np.uint8, W * H * 4), want_last)
+    # a memset between frames: after frame A, before frame B (which writes elsewhere)
+    other = g.DeviceBuffer(ctx, W * H * 4)
+    render_spec(sp, pose(W, H, 1), out)
+    check(lib().gs_memset(ctx.handle, out.ptr, 0, W * H * 4), ctx.handle)
+    render_spec(sp, pose(W, H, 2), other)
+    ctx.sync()
+    assert not out.download(np.uint8, W * H * 4).any()
+    # the memset's target written again by the next frame: that frame's image
+    render_spec(sp, pose(W, H, 3), out)
+    ctx.sync()
+    render_sync(sp, pose(W, H, 3), ref)
+    assert np.array_equal(out.download(np.uint8, W * H * 4), ref.download(np.uint8, W * H * 4))
+    ctx.close()
+
+
+def test_one_and_two_lanes_identical():
+    W, H = 512, 384
+    imgs = {}
+    for lanes in (1, 2):
+        ctx = g.Context(0)
+        ctx.set_lanes(lanes)
+        means, rot, sc, op, col = c2_scene()
+        sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+        outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(5)]
+        render_sync(sp, pose(W, H, 0), outs[0])
+        for k in range(5):
+            render_spec(sp, pose(W, H, k), outs[k])
+        ctx.sync()
+        imgs[lanes] = [o.download(np.uint8, W * H * 4) for o in outs]
+        ctx.close()
+    for a, b in zip(imgs[1], imgs[2]):
+        assert np.array_equal(a, b)
+    with pytest.raises(g.GsError):
+        ctx = g.Context(0)
+        try:
+            ctx.set_lanes(3)
+        finally:
+            ctx.close()
