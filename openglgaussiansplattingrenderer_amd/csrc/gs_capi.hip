@@ -72,6 +72,7 @@ struct gs_ctx {
     int n = 0;
     int64_t V = 0, D = 0, E = 0;  // of the newest frame whose counts the host has seen
     uint32_t flags = 0;
+    bool rec_packed = true;  // the newest frame's emission records are 8-byte packed
     // Frames in flight.  Each frame takes the next of kRing slots: its hipEvent set, its
     // pinned (V, D) and -- for a frame enqueued without a host round trip ("speculative":
     // the entry count stays on the device, kernels are sized by the entry capacity) -- what is
@@ -769,6 +770,7 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     ctx->flags = flags;
     gs::PreParams P = pre_params(u, flags, n);
     P.sh = sh ? 1 : 0;
+    ctx->rec_packed = gs::rec_packed(P);
     // camera position = -R^T t of the view matrix (column-major, view[4c + r])
     for (int c = 0; c < 3; ++c)
         P.campos[c] = -(u->view[4 * c + 0] * u->view[12] + u->view[4 * c + 1] * u->view[13] +
@@ -784,7 +786,7 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
 }
 
 int enqueue_emit(gs_ctx *ctx) {
-    gs::launch_emit(ctx->L->stream, ctx->n, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
+    gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
                     fev(ctx, 3));
     GS_HIP(ctx, hipGetLastError());
     return GS_OK;
@@ -1014,10 +1016,16 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     size_t avail = 0, esz = 4;
     // preprocess writes the blend records and boxes of splats with entries only; the rows of
     // the others read as the values a culled splat gets (zeros, the empty box)
+    // culled(ty[r]): splat r has no entries (read after the stream sync)
+    auto culled = [&](int32_t v) { return ctx->rec_packed ? v >= 0 : v < 0; };
     auto has_entries = [&](size_t rows, std::vector<int32_t> &ty) -> int {
         ty.resize(rows);
-        GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->L->rec + 4, sizeof(int4), 4, rows,
-                                     hipMemcpyDeviceToHost, ctx->L->stream));
+        if (ctx->rec_packed)  // word 1 of the 8-byte record, bit 31 set: has entries
+            GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->L->rec + 4, 8, 4, rows,
+                                         hipMemcpyDeviceToHost, ctx->L->stream));
+        else
+            GS_HIP(ctx, hipMemcpy2DAsync(ty.data(), 4, (const char *)ctx->L->rec + 4, sizeof(int4), 4, rows,
+                                         hipMemcpyDeviceToHost, ctx->L->stream));
         return GS_OK;
     };
     switch (what) {
@@ -1039,7 +1047,7 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
             if (int rc = has_entries(rows, ty)) return rc;
             GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
             for (size_t r = 0; r < rows; ++r)
-                if (ty[r] < 0) std::fill(tmp.begin() + r * comps, tmp.begin() + (r + 1) * comps, 0.0f);
+                if (culled(ty[r])) std::fill(tmp.begin() + r * comps, tmp.begin() + (r + 1) * comps, 0.0f);
             std::memcpy(host_dst, tmp.data(), count * 4);
         }
         return GS_OK;
@@ -1055,7 +1063,7 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
             GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
             const float inf = std::numeric_limits<float>::infinity();
             for (size_t r = 0; r < rows; ++r)
-                if (ty[r] < 0) {
+                if (culled(ty[r])) {
                     tmp[4 * r] = inf;
                     tmp[4 * r + 1] = -inf;
                     tmp[4 * r + 2] = inf;

@@ -102,7 +102,7 @@ struct alignas(32) SplatDraw {
 struct FrameDev {
     SplatDraw *sd;
     float4 *cullbox;   // conservative pixel box of the alpha >= 1/255 region
-    int4 *rec;         // z01 bits, tileX, tileY (-1: no entries), packed rect
+    int4 *rec;         // emission records: 8-byte packed (rec_packed) or (z01 bits, tileX, tileY (-1: no entries), rect)
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
     uint32_t *totals;  // [0]=V [1]=D
     uint32_t *h_totals;  // mapped pinned host copy of (V, D) for this frame, or null
@@ -112,7 +112,8 @@ int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block s
 // start / stop: optional hipEvents recorded on the dispatch packets (stage timing)
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);
-void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preprocess) fits this frame
+void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
                  hipEvent_t start, hipEvent_t stop);
 // E entries, or min(E, dev_count[0] + dev_count[1]) when dev_count is given; counts must be
 // zero on entry and are left zero

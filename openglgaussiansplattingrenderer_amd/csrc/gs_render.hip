@@ -145,6 +145,23 @@ __device__ __forceinline__ float sh_channel(const float *sh, size_t n, size_t i,
 constexpr int kPer = 4;
 constexpr int kSplatsPerBlock = kPer * kBlock;  // 1024
 
+// The emission record of splat i (rec): z01 bits, main tile, tile rect, "has entries".  PACK: 8
+// bytes -- z01 bits, then tileX | tileY << 5 | minX << 10 | maxX << 15 | minY << 20 | maxY << 25 |
+// has << 31 (every field fits 5 bits whenever the tile sizes are >= 1 px: tileX <= W / int(W/16)
+// <= 31, min clamped to 16, max <= 15); else (reference mode below 16 px, tile size 0, where the
+// main tile saturates) the 16-byte (z01 bits, tileX, tileY, rect bytes) form.
+__device__ __forceinline__ uint32_t pack_rec(int tileX, int tileY, uint32_t rp) {
+    return (uint32_t)tileX | ((uint32_t)tileY << 5) | ((rp & 0xffu) << 10) | (((rp >> 8) & 0xffu) << 15) |
+           (((rp >> 16) & 0xffu) << 20) | ((rp >> 24) << 25) | 0x80000000u;
+}
+__device__ __forceinline__ int4 unpack_rec(uint2 r) {
+    if (!(r.y >> 31)) return make_int4((int)r.x, -1, -1, 0);
+    const uint32_t w = r.y;
+    const uint32_t rp = ((w >> 10) & 31u) | (((w >> 15) & 31u) << 8) | (((w >> 20) & 31u) << 16) | (((w >> 25) & 31u) << 24);
+    return make_int4((int)r.x, (int)(w & 31u), (int)((w >> 5) & 31u), (int)rp);
+}
+
+template <bool PACK>
 __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_wave[kBlock / 64];
     uint32_t n_main = 0, n_dup = 0;
@@ -271,7 +288,11 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
                                     sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
         }
         }
-        fr.rec[i] = rc;
+        if (PACK)
+            reinterpret_cast<uint2 *>(fr.rec)[i] =
+                make_uint2((uint32_t)rc.x, rc.y >= 0 ? pack_rec(rc.y, rc.z, (uint32_t)rc.w) : 0u);
+        else
+            fr.rec[i] = rc;
     }
     }
     // block sums of (main, dup) for the emission offsets
@@ -355,6 +376,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 
 // Entries at positions >= cap are not written (a frame enqueued before its entry count is
 // known on the host; the host detects the overflow from the totals and renders again).
+template <bool PACK>
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
                                                  uint32_t *__restrict__ vals, uint32_t cap) {
     __shared__ uint32_t s_wave[kBlock / 64];
@@ -368,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
     for (int it = 0; it < kPer; ++it) {
         const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
         int4 rc = make_int4(0, -1, -1, 0);
-        if (i < n) rc = fr.rec[i];
+        if (i < n) rc = PACK ? unpack_rec(reinterpret_cast<const uint2 *>(fr.rec)[i]) : fr.rec[i];
         const bool has = rc.y >= 0;
         const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
         const int tileX = rc.y, tileY = rc.z;
@@ -1002,19 +1024,24 @@ int preprocess_blocks(int n) { return (n + kSplatsPerBlock - 1) / kSplatsPerBloc
 
 // Stage timing rides on the dispatch packets (hipExtLaunchKernelGGL start / stop events): a
 // separate hipEventRecord costs an idle gap of several microseconds on the stream.
+bool rec_packed(const PreParams &P) { return P.clean || (P.W >= 16 && P.H >= 16); }
+
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start) {
     const int nb = preprocess_blocks(P.n);
-    if (nb > 0) hipExtLaunchKernelGGL(k_preprocess, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+    if (nb <= 0) return;
+    if (rec_packed(P)) hipExtLaunchKernelGGL(k_preprocess<true>, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+    else hipExtLaunchKernelGGL(k_preprocess<false>, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
     hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, start, stop, 0, fr, nblocks);
 }
 
-void launch_emit(hipStream_t s, int n, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
                  hipEvent_t start, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(k_emit, dim3(std::max(preprocess_blocks(n), 1)), dim3(kBlock), 0, s, start, stop, 0, n, fr,
-                          keys, vals, cap);
+    const dim3 grid(std::max(preprocess_blocks(n), 1));
+    if (packed) hipExtLaunchKernelGGL(k_emit<true>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap);
+    else hipExtLaunchKernelGGL(k_emit<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap);
 }
 
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,

@@ -81,7 +81,8 @@ def test_golden_configs(ctx, golden_dir, name, mode, flags):
     assert_image_tol(rf["image"], z[f"{mode}_image"], f"{name}/{mode}/fast")
 
 
-@pytest.mark.parametrize("W,H,n", [(1920, 1080, 20_000), (3840, 2160, 4_000), (1000, 600, 15_000)])
+@pytest.mark.parametrize("W,H,n", [(1920, 1080, 20_000), (3840, 2160, 4_000), (1000, 600, 15_000),
+                                   (12, 40, 3_000)])  # 12 px: reference tile width 0 (16-byte records)
 @pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
 def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags):
     """1080p / 4K / odd sizes: Q4 (int vs float tile dims), Q5 (unclamped main tile),
