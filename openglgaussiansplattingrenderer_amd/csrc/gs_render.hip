@@ -303,16 +303,19 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
 }
 
 // exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1].
-// One workgroup; each thread owns 16 consecutive sums per round (independent loads issued
-// together), so a round costs one memory round trip instead of one per 1024 sums.
-constexpr int kScanPer = 16;
-__global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblocks) {
-    __shared__ uint32_t s_w0[16], s_w1[16];
+// One workgroup of 256 (a small workgroup finds room on a CU beside the previous frame's blend,
+// which occupies most wave slots while this runs; 1024 threads waited ~50 us for one CU to
+// drain); each thread owns 24 consecutive sums per round (independent loads issued together):
+// one round covers 6144 block sums = 6.3M splats.
+constexpr int kScanThreads = 256, kScanPer = 24;
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, int nblocks) {
+    constexpr int W = kScanThreads / 64;
+    __shared__ uint32_t s_w0[W], s_w1[W];
     __shared__ uint32_t s_carry[2];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry[0] = s_carry[1] = 0;
     __syncthreads();
-    for (int base = 0; base < nblocks; base += 1024 * kScanPer) {
+    for (int base = 0; base < nblocks; base += kScanThreads * kScanPer) {
         const int i0 = base + threadIdx.x * kScanPer;
         uint2 v[kScanPer];
 #pragma unroll
@@ -330,7 +333,8 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(FrameDev fr, int nblock
         }
         __syncthreads();
         uint32_t o0 = s_carry[0], o1 = s_carry[1], t0 = 0, t1 = 0;
-        for (int w = 0; w < 16; ++w) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
             o0 += (w < wid) ? s_w0[w] : 0u;
             o1 += (w < wid) ? s_w1[w] : 0u;
             t0 += s_w0[w];
@@ -1034,7 +1038,7 @@ void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, co
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, start, stop, 0, fr, nblocks);
+    hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, nblocks);
 }
 
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,

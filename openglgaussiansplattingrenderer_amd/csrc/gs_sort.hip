@@ -86,6 +86,24 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_wave
     return off + inc - v;
 }
 
+// the same, also returning the block total
+template <int W>
+__device__ __forceinline__ uint32_t block_excl_scan_tot(uint32_t v, uint32_t *s_wave, uint32_t *total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_wave[wid] = inc;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        off += (w < wid) ? s_wave[w] : 0u;
+        tot += s_wave[w];
+    }
+    __syncthreads();
+    *total = tot;
+    return off + inc - v;
+}
+
 // element count: n, or min(n, cnt[0] + cnt[1]) when the count lives on the device (a frame
 // enqueued without a host round trip; the grid is sized for n, the capacity)
 __device__ __forceinline__ uint32_t elem_count(uint32_t n, const uint32_t *cnt) {
@@ -151,80 +169,67 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     }
 }
 
-// tile bins from the tile counts (one workgroup of 1024): bins[t] = inclusive prefix, and the
+// tile bins from the tile counts (one workgroup of 256): bins[t] = inclusive prefix, and the
 // draw's tile order bins[256 + r] = the tile with the r-th longest list (ties by index); the
 // counts are cleared for the next frame
 __device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w) {
     __shared__ uint32_t s_c[kRadix];
-    __shared__ uint32_t s_part[4][kRadix];
-    const int t = threadIdx.x & (kRadix - 1), q = threadIdx.x >> 8;
-    if (q == 0) {
-        uint32_t c = 0;
+    const int t = threadIdx.x;
+    uint32_t v = 0;
 #pragma unroll
-        for (int k = 0; k < kTileCopies; ++k) {
-            c += counts[k * kRadix + t];
-            counts[k * kRadix + t] = 0;
-        }
-        s_c[t] = c;
+    for (int k = 0; k < kTileCopies; ++k) {
+        v += counts[k * kRadix + t];
+        counts[k * kRadix + t] = 0;
     }
-    __syncthreads();
-    const uint32_t v = s_c[t];
-    // rank = #tiles ahead of t: longer, or as long with a smaller index (4 quarters of u)
+    s_c[t] = v;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_tot<4>(v, s_w, &tot);  // (its barriers also publish s_c)
+    bins[t] = ex + v;
+    // rank = #tiles ahead of t: longer, or as long with a smaller index
     uint32_t r = 0;
-#pragma unroll 16
-    for (int u = 64 * q; u < 64 * q + 64; ++u) {
+#pragma unroll 32
+    for (int u = 0; u < kRadix; ++u) {
         const uint32_t c = s_c[u];
         r += (c > v || (c == v && u < t)) ? 1u : 0u;
     }
-    s_part[q][t] = r;
-    // inclusive prefix of the counts over the first 4 waves
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t inc = wave_incl_scan(q == 0 ? v : 0u);
-    if (lane == 63 && wid < 4) s_w[wid] = inc;
-    __syncthreads();
-    if (q == 0) {
-        uint32_t off = 0;
-        for (int w = 0; w < wid; ++w) off += s_w[w];
-        bins[t] = off + inc;
-        bins[kRadix + s_part[0][t] + s_part[1][t] + s_part[2][t] + s_part[3][t]] = (uint32_t)t;
-    }
+    bins[kRadix + r] = (uint32_t)t;
 }
 
-// one block per digit: exclusive scan of that digit's per-tile counts (the tiles holding
-// elements; rows are nb long), row total.  With bins != null, block 256 computes the tile
-// bins from tile_counts instead (bins_scan).
-__global__ __launch_bounds__(1024) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
-                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
-                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
-                                                    uint32_t *__restrict__ bins) {
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_carry;
+// One workgroup of 256 per digit (a small workgroup finds room on a CU beside the previous
+// frame's blend; 1024-thread ones waited for a CU to drain): exclusive scan of that digit's
+// per-tile counts (the tiles holding elements; rows are nb long), row total.  Each thread owns
+// 16 consecutive counts per round, so a round (4096 tiles = 16.7M keys) costs one memory round
+// trip.  With bins != null, block kRadix computes the tile bins from tile_counts instead.
+__global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
+                                                   const uint32_t *__restrict__ cnt, uint32_t tile,
+                                                   uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
+                                                   uint32_t *__restrict__ bins) {
+    constexpr int kPer = 16;
+    __shared__ uint32_t s_w[4];
     if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
         bins_scan(tile_counts, bins, s_w);
         return;
     }
     const uint32_t nb = (elem_count(n_max, cnt) + tile - 1) / tile;
     uint32_t *row = hist + (size_t)blockIdx.x * nb_stride;
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_carry = 0;
-    __syncthreads();
-    for (uint32_t b = 0; b < nb; b += 1024) {
-        const uint32_t i = b + threadIdx.x;
-        const uint32_t v = (i < nb) ? row[i] : 0u;
-        const uint32_t inc = wave_incl_scan(v);
-        if (lane == 63) s_w[wid] = inc;
-        __syncthreads();
-        uint32_t off = s_carry, tot = 0;
-        for (int w = 0; w < 16; ++w) {
-            off += (w < wid) ? s_w[w] : 0u;
-            tot += s_w[w];
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < nb; b += 256 * kPer) {
+        const uint32_t i0 = b + threadIdx.x * kPer;
+        uint32_t v[kPer], a = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) v[k] = (i0 + k < nb) ? row[i0 + k] : 0u;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) a += v[k];
+        uint32_t tot;
+        uint32_t off = carry + block_excl_scan_tot<4>(a, s_w, &tot);
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            if (i0 + k < nb) row[i0 + k] = off;
+            off += v[k];
         }
-        if (i < nb) row[i] = off + inc - v;
-        __syncthreads();
-        if (threadIdx.x == 0) s_carry += tot;
-        __syncthreads();
+        carry += tot;
     }
-    if (threadIdx.x == 0) row_total[blockIdx.x] = s_carry;
+    if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
 }
 
 template <int W>
@@ -401,7 +406,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     uint32_t *tile_counts = sc.row_total + kRadix;
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
         if (start) (void)hipEventRecord(start, s);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + 1), dim3(1024), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
                            tile_counts, bins);
         if (stop) (void)hipEventRecord(stop, s);
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
@@ -421,7 +426,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
             hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
                                   (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
         const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(1024), 0, s, sc.hist, nb, (uint32_t)n,
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
                            dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
         if (big)
             hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
