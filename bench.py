@@ -177,6 +177,8 @@ def main():
     ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
                     help="frames in flight per GPU (gs_ctx_set_lanes): 2 overlaps frame k+1's preprocess / "
                          "emission / sort with frame k's blend")
+    ap.add_argument("--view", type=int, default=None,
+                    help="C5 pose index to render (default: this rank's, main pose + rotateRight(45 deg * k))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -197,7 +199,8 @@ def main():
         f_dc = ((sp.colours[:, :3] / 255.0 - 0.5) / 0.28209479177387814).astype(np.float32)
         sp.set_sh(f_dc, rng.normal(0, 0.1, (sp.numSplats, 45)).astype(np.float32))
         data_desc += "; seeded synthetic f_rest N(0, 0.1^2)"
-    u = camera_for_rank(W, H, rank).uniforms()
+    view = rank if args.view is None else args.view
+    u = camera_for_rank(W, H, view).uniforms()
 
     for _ in range(args.warmup):
         sp.render_uniforms(u)
