@@ -174,6 +174,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
         float4 box = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
         int4 rc = make_int4(0, -1, -1, 0);
+        float lg = 0.0f;  // ln(255 o) for the culling quantities below (hardware log, see there)
         do {
             // :77-78
             float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
@@ -251,16 +252,22 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
             // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
             // culling an entry outside the box never changes a pixel.
+            // The box and the pre-exp threshold only cull (they never enter a pixel's
+            // arithmetic) and carry margins far above hardware-instruction error (0.05 in ln,
+            // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
+            // v_sqrt instead of the correctly rounded library sequences.
             const float A = co.x, B = co.y, Cq = co.z;
-            const float tau = logf(255.0f * opac) + 0.05f;
+            lg = __logf(255.0f * opac);
+            const float tau = lg + 0.05f;
             if (!(tau > 0.0f)) {
                 // never reaches 1/255 anywhere: empty box (stays +inf,-inf)
             } else {
                 const float detQ = A * Cq - B * B;
                 const float trq = A + Cq;
                 if (A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ) {
-                    const float hx = sqrtf(2.0f * tau * Cq / detQ) * 1.02f + 1.0f;
-                    const float hy = sqrtf(2.0f * tau * A / detQ) * 1.02f + 1.0f;
+                    const float rq = __builtin_amdgcn_rcpf(detQ);
+                    const float hx = __builtin_amdgcn_sqrtf(2.0f * tau * Cq * rq) * 1.02f + 1.0f;
+                    const float hy = __builtin_amdgcn_sqrtf(2.0f * tau * A * rq) * 1.02f + 1.0f;
                     box = make_float4(sx - hx, sx + hx, sy - hy, sy + hy);
                 } else {
                     box = make_float4(-__builtin_inff(), __builtin_inff(), -__builtin_inff(), __builtin_inff());
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // the blend record, box and (GS_FLAG_SH) colour are read only through entries: written
         // for the splats that have some (gs_frame_read shows the others as culled)
         if (rc.y >= 0) {
-        float thr = -logf(255.0f * co.w) - 1.0e-3f;
+        float thr = -lg - 1.0e-3f;
         if (thr != thr) thr = -__builtin_inff();
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
         fr.cullbox[i] = box;
