@@ -904,7 +904,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 s_col[pix] = col;
                 sat = max(sat, __float_as_uint(col.w));  // :129-133
             };
-            if ((uint32_t)lane < nev) event(lane);
+            // every lane runs an event (no exec mask around it): lanes >= nev repeat the last
+            // one, reading the same old state and writing the same new state to one address
+            event(min((uint32_t)lane, nev - 1u));
             if (nev > 64)  // uniform, rare: more events than lanes
                 for (uint32_t e = lane + 64; e < nev; e += 64) event(e);
             if (ballot(sat >= __float_as_uint(0.99f))) {  // uniform, rare: a pixel saturated -- refresh the done masks
