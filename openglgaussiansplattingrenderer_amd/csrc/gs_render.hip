@@ -169,7 +169,13 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
     for (int it = 0; it < kPer; ++it) {
     const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
     if (i < P.n) {
+        // all ten planes in one round trip (the covariance and opacity of culled splats are
+        // read for nothing: 28 B of 40 for 24 % of C3's splats, cheaper than a second trip)
         const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
+        const size_t n = (size_t)P.n;
+        const float c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
+        const float c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
+        const float opac = sc.opacity[i];
         float2 m2 = make_float2(0.f, 0.f);
         float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
         float4 box = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
@@ -195,9 +201,6 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             if (P.clean && !(sz >= 0.0f && sz <= 1.0f)) break;  // clean: near/far cull (Q6)
             m2 = make_float2(sx, sy);
             // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
-            const size_t n = (size_t)P.n;
-            const float c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
-            const float c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
             const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
             const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
                             {P.view[8], P.view[9], P.view[10]}}};
@@ -223,7 +226,6 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             if (det == 0) break;                   // Q7: entry omitted
             if (P.clean && !(det > 0.0f)) break;
             const float inv = 1.0f / det;
-            const float opac = sc.opacity[i];
             co = make_float4(cc * inv, -cb * inv, ca * inv, opac);
             // :139-149
             const float middle = (cc + ca) * 0.5f;
