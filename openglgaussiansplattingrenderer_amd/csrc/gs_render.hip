@@ -306,8 +306,12 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
     }
     // block sums of (main, dup) for the emission offsets
     uint32_t tot_main, tot_dup;
-    block_excl_scan256(n_main, s_wave, &tot_main);
-    block_excl_scan256(n_dup, s_wave, &tot_dup);
+    {  // one scan of both: mains in the low 11 bits (<= 1024 per block), duplicates above (<= 261120)
+        uint32_t tot;
+        block_excl_scan256(n_main | (n_dup << 11), s_wave, &tot);
+        tot_main = tot & 0x7ffu;
+        tot_dup = tot >> 11;
+    }
     if (threadIdx.x == 0) fr.blocksum[blockIdx.x] = make_uint2(tot_main, tot_dup);
 }
 
@@ -414,9 +418,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             n_main = 1;
             n_dup = (uint32_t)(rectCount - mainInRect);
         }
-        uint32_t t0, t1;
-        const uint32_t pm = block_excl_scan256(n_main, s_wave, &t0);
-        const uint32_t pd = block_excl_scan256(n_dup, s_wave, &t1);
+        // one scan of both: mains in the low 16 bits (<= 256 per item), duplicates above (<= 65280)
+        uint32_t tp;
+        const uint32_t pp = block_excl_scan256(n_main | (n_dup << 16), s_wave, &tp);
+        const uint32_t pm = pp & 0xffffu, pd = pp >> 16, t0 = tp & 0xffffu, t1 = tp >> 16;
         if (has) {
             // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
             const uint32_t mpos = carry_m + pm;
