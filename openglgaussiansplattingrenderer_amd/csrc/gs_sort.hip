@@ -110,6 +110,18 @@ __device__ __forceinline__ uint32_t elem_count(uint32_t n, const uint32_t *cnt) 
     return cnt ? min(n, cnt[0] + cnt[1]) : n;
 }
 
+// Tile of a workgroup: workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD
+// b % 8), so XCD x is given the contiguous tiles [x * per, (x + 1) * per): neighbouring
+// columns of hist[digit][tile] are then written and read through one L2 instead of eight
+// (the upsweep's 4-byte column stores wrote back as partial lines from every XCD).  The grid
+// is 8 * ceil(capacity tiles / 8) workgroups; the mapping uses the live tiles (the count read
+// on the device), so every XCD gets work; workgroups mapped past them return.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t live) {
+    const uint32_t per = (live + 7) / 8, j = blockIdx.x >> 3;
+    return j < per ? (blockIdx.x & 7u) * per + j : 0xffffffffu;  // (>= live: no tile)
+}
+__host__ __device__ constexpr uint32_t xcd_grid(uint32_t nb) { return 8 * ((nb + 7) / 8); }
+
 // W waves per workgroup, tile = W * 1024 keys (the pass-0 sort uses W = 8: its random low
 // digits leave short runs per tile, so a larger tile doubles the scatter's write runs)
 // tile_counts != null: also countBins.glsl:20-31 -- tile_counts[int(key)] += 1 for int(key) in
@@ -121,7 +133,9 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ tile_counts) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems;
     const uint32_t n = elem_count(n_max, cnt);
-    if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count (never scanned)
+    const uint32_t live = (n + kTile - 1) / kTile;
+    const uint32_t tile = xcd_tile(live);
+    if (tile >= live) return;  // uniform: tile beyond the count (never scanned)
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
@@ -129,9 +143,9 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) s_cnt[i] = s_tiles[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t base = blockIdx.x * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
+    const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems];
-    if (blockIdx.x * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
+    if (tile * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
         const uint32_t *p = keys + base;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) kk[k] = p[k * 64];
@@ -162,7 +176,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         const uint4 c1 = *reinterpret_cast<const uint4 *>(p + 4);
         return (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
     };
-    hist[(size_t)d * nb + blockIdx.x] = sum8(&s_cnt[d * kRep]);
+    hist[(size_t)d * nb + tile] = sum8(&s_cnt[d * kRep]);
     if (tile_counts) {
         const uint32_t c = sum8(&s_tiles[d * kRep]);
         if (c) atomicAdd(&tile_counts[(blockIdx.x % kTileCopies) * kRadix + d], c);
@@ -240,7 +254,9 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ row_total) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
     const uint32_t n = elem_count(n_max, cnt);
-    if (blockIdx.x * (uint32_t)kTile >= n) return;  // uniform: tile beyond the count
+    const uint32_t live = (n + kTile - 1) / kTile;
+    const uint32_t tile = xcd_tile(live);
+    if (tile >= live) return;  // uniform: tile beyond the count
     __shared__ uint32_t s_cnt[kWaves][kRadix];  // running per-wave counts -> per-wave exclusive offsets
     __shared__ uint32_t s_start[kRadix];        // block-local start of each digit
     __shared__ int32_t s_gbase[kRadix];         // global position of local slot 0 of each digit
@@ -251,7 +267,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t tile0 = blockIdx.x * (uint32_t)kTile;
+    const uint32_t tile0 = tile * (uint32_t)kTile;
     const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems], vv[kItems];
     if (tile0 + kTile <= n) {  // uniform: full tile, immediate offsets
@@ -313,7 +329,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         const uint32_t gdig = block_excl_scan<W>(dig ? row_total[d] : 0u, s_wave);  // digit base, whole array
         if (dig) {
             s_start[d] = start;
-            s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + blockIdx.x]) - (int32_t)start;
+            s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + tile]) - (int32_t)start;
         }
     }
     __syncthreads();
@@ -420,19 +436,19 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         if (big)
-            hipExtLaunchKernelGGL(k_upsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin,
+            hipExtLaunchKernelGGL(k_upsweep<kWaveBig>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin,
                                   (uint32_t)n, dev_count, shift, sc.hist, nb, bins ? tile_counts : nullptr);
         else
-            hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
+            hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
                                   (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
         const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
                            dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
         if (big)
-            hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(nb), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
+            hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
                                   kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         else
-            hipExtLaunchKernelGGL(k_downsweep<kWaveSmall>, dim3(nb), dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin,
+            hipExtLaunchKernelGGL(k_downsweep<kWaveSmall>, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin,
                                   vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         std::swap(kin, kout);
         std::swap(vin, vout);

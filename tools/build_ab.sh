@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build the committed HEAD's library as lib/libgsplat_hip_old.so beside the working tree's
+# lib/libgsplat_hip.so (for tools/ab_lib.sh on the GPU box).  Run from the repo root.
+set -e
+M="make -s -j8 -C openglgaussiansplattingrenderer_amd ARCH=gfx950"
+git stash -q
+$M
+cp openglgaussiansplattingrenderer_amd/lib/libgsplat_hip.so /tmp/libgsplat_hip_old.so
+git stash pop -q
+$M
+cp /tmp/libgsplat_hip_old.so openglgaussiansplattingrenderer_amd/lib/libgsplat_hip_old.so
