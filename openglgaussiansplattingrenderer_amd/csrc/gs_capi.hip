@@ -33,7 +33,7 @@ struct Lane {
     gs::SplatDraw *sd = nullptr;
     float4 *col = nullptr;  // per-frame colours of GS_FLAG_SH frames
     int col_cap = 0;
-    float4 *cullbox = nullptr;
+    uint2 *cullbox = nullptr;
     int4 *rec = nullptr;
     uint2 *blocksum = nullptr;
     uint32_t *totals = nullptr;      // device [4]
@@ -1057,18 +1057,24 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         const size_t rows = (count + 3) / 4;
         if (rows) {
             std::vector<float> tmp(rows * 4);
+            std::vector<uint32_t> packed(rows * 2);
             std::vector<int32_t> ty;
-            GS_HIP(ctx, hipMemcpyAsync(tmp.data(), ctx->L->cullbox, rows * 16, hipMemcpyDeviceToHost, ctx->L->stream));
+            GS_HIP(ctx, hipMemcpyAsync(packed.data(), ctx->L->cullbox, rows * 8, hipMemcpyDeviceToHost, ctx->L->stream));
             if (int rc = has_entries(rows, ty)) return rc;
             GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
             const float inf = std::numeric_limits<float>::infinity();
-            for (size_t r = 0; r < rows; ++r)
+            for (size_t r = 0; r < rows; ++r) {  // biased 16-bit pixel bounds -> (x0, x1, y0, y1)
+                for (int c = 0; c < 2; ++c) {
+                    tmp[4 * r + 2 * c] = (float)((int)(packed[2 * r + c] & 0xffffu) - 32768);
+                    tmp[4 * r + 2 * c + 1] = (float)((int)(packed[2 * r + c] >> 16) - 32768);
+                }
                 if (culled(ty[r])) {
                     tmp[4 * r] = inf;
                     tmp[4 * r + 1] = -inf;
                     tmp[4 * r + 2] = inf;
                     tmp[4 * r + 3] = -inf;
                 }
+            }
             std::memcpy(host_dst, tmp.data(), count * 4);
         }
         return GS_OK;

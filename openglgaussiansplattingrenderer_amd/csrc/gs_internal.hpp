@@ -101,7 +101,7 @@ struct alignas(32) SplatDraw {
 };
 struct FrameDev {
     SplatDraw *sd;
-    float4 *cullbox;   // conservative pixel box of the alpha >= 1/255 region
+    uint2 *cullbox;    // conservative pixel box of the alpha >= 1/255 region (int16 bounds, pack_box)
     int4 *rec;         // emission records: 8-byte packed (rec_packed) or (z01 bits, tileX, tileY (-1: no entries), rect)
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
     uint32_t *totals;  // [0]=V [1]=D

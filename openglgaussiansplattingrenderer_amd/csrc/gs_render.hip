@@ -161,6 +161,18 @@ __device__ __forceinline__ int4 unpack_rec(uint2 r) {
     return make_int4((int)r.x, (int)(w & 31u), (int)((w >> 5) & 31u), (int)rp);
 }
 
+// The cull box as 16-bit pixel bounds biased by 32768 (unsigned), 8 bytes:
+// (floor x0 | ceil x1 << 16, floor y0 | ceil y1 << 16), clamped to [-32768, 32767] -- never
+// smaller than the float box, so the cull stays conservative (an empty box stays empty: +inf /
+// -inf clamp to 32767 / -32768; NaN bounds open up).  The bias makes the blend's tests plain
+// unsigned compares (kBoxBias).
+constexpr int kBoxBias = 32768;
+__device__ __forceinline__ uint2 pack_box(const float4 &b) {
+    auto lo = [](float v) { return (uint32_t)((int)fminf(fmaxf(floorf(v), -32768.0f), 32767.0f) + kBoxBias); };  // NaN -> 0
+    auto hi = [](float v) { return (uint32_t)((int)fmaxf(fminf(ceilf(v), 32767.0f), -32768.0f) + kBoxBias); };   // NaN -> 65535
+    return make_uint2(lo(b.x) | (hi(b.y) << 16), lo(b.z) | (hi(b.w) << 16));
+}
+
 template <bool PACK>
 __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_wave[kBlock / 64];
@@ -285,7 +297,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         float thr = -lg - 1.0e-3f;
         if (thr != thr) thr = -__builtin_inff();
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
-        fr.cullbox[i] = box;
+        fr.cullbox[i] = pack_box(box);
         if (P.sh) {  // GS_FLAG_SH: this frame's colour
             float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
             const float len = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -646,7 +658,7 @@ static_assert(offsetof(SplatDraw, thr) == offsetof(SurvData, thr), "SurvData mir
 template <bool FAST_EXP, bool STATS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
-                                             const float4 *__restrict__ cullbox,
+                                             const uint2 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
                                              uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
     // pixel state, pixel id = 4*lane + slot; a pixel is done (:129-133) iff its w >= 0.99 (pixels
@@ -740,6 +752,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // the cull rectangle: the sub-block, then the bounding box of its active pixels (a done
     // pixel never blends, so a splat missing every active pixel is skipped exactly)
     float rx0 = bx0, rx1 = bx1, ry0 = by0, ry1 = by1;
+    // the same, biased as the packed box bounds (pack_box)
+    uint32_t irx0 = x0 + kBoxBias, irx1 = x1 - 1 + kBoxBias, iry0 = y0 + kBoxBias, iry1 = y1 - 1 + kBoxBias;
 
     // Sparse phase: once at most 64 pixels are active, each lane takes one of them (its state
     // in registers for the survivors of a chunk) and a survivor costs one power / exp / blend
@@ -777,6 +791,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         rx1 = uni(mxx);
         ry0 = uni(mny);
         ry1 = uni(mxy);
+        irx0 = (uint32_t)((int)rx0 + kBoxBias);
+        irx1 = (uint32_t)((int)rx1 + kBoxBias);
+        iry0 = (uint32_t)((int)ry0 + kBoxBias);
+        iry1 = (uint32_t)((int)ry1 + kBoxBias);
         sparse = true;
     };
     // blocks with few pixels in the image start sparse
@@ -791,7 +809,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // copy makes the compiler wait for all outstanding loads (vmcnt is in-order) and the
     // pipeline collapses to one memory latency per step.
     uint32_t Vi[2], Vb[2];      // indices: as loaded / riding with the box gather
-    float4 Bx[2];               // boxes
+    uint2 Bx[2];                // boxes (int16 pixel bounds, pack_box)
     uint64_t K[2];              // survivors of the box test (then of the exact cull)
     SurvData Dd[2];             // survivor data (lane-held; other lanes hold copies)
     SurvRgb Dc[2];              // survivor colour
@@ -804,15 +822,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         return reinterpret_cast<decltype(base)>(reinterpret_cast<const char *>(base) + byte_off);
     };
     auto load_idx = [&](int base, uint32_t &v) { v = *at(vals, (uint32_t)min(base + lane, jmax) << 2); };
-    auto gather_box = [&](uint32_t v, uint32_t &vb, float4 &bx) {
+    auto gather_box = [&](uint32_t v, uint32_t &vb, uint2 &bx) {
         vb = v;
-        bx = *at(cullbox, v << 4);
+        bx = *at(cullbox, v << 3);
     };
-    auto test_and_gather = [&](int cbase, uint32_t v, const float4 &bx, uint64_t &keep, SurvData &d,
+    auto test_and_gather = [&](int cbase, uint32_t v, const uint2 &bx, uint64_t &keep, SurvData &d,
                                SurvRgb &c) {
         // bitwise, not short-circuit: no branch around the compares
         const bool in = (cbase + lane < end) &
-                        (!cull | ((bx.x <= rx1) & (bx.y >= rx0) & (bx.z <= ry1) & (bx.w >= ry0)));
+                        (!cull | (((bx.x & 0xffffu) <= irx1) & ((bx.x >> 16) >= irx0) & ((bx.y & 0xffffu) <= iry1) &
+                                  ((bx.y >> 16) >= iry0)));
         keep = ballot(in);
         // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
         const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
