@@ -40,6 +40,7 @@ struct Lane {
     // entries
     int64_t e_cap = 0;
     uint32_t *keys = nullptr, *vals = nullptr;
+    bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     gs::SortScratch sort;
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
@@ -786,6 +787,7 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
 }
 
 int enqueue_emit(gs_ctx *ctx) {
+    ctx->L->keys_sorted = true;  // emission order, as gs_frame_read shows it before gs_sort
     gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
                     fev(ctx, 3));
     GS_HIP(ctx, hipGetLastError());
@@ -795,10 +797,14 @@ int enqueue_emit(gs_ctx *ctx) {
 // E entries, or (count != null) min(E, count[0] + count[1]) read on the device
 // with_bins: the tile bins (gs_compute_bins' output) come from the sort's own histogram read;
 // the bins stage is then empty (its timing event follows the sort's)
+// A frame sort with bins leaves the keys unsorted (the blend reads the values and the bins
+// only) when the splat ids fit 24 bits; gs_frame_read(GS_READ_KEYS) then sorts again.
 int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false) {
+    const bool keys_out = !with_bins || ctx->n > (1 << 24);
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr))
+                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out))
         return set_error(ctx, rc, ctx->err);
+    ctx->L->keys_sorted = keys_out;
     if (with_bins)
         if (hipEvent_t e = fev(ctx, 6)) GS_HIP(ctx, hipEventRecord(e, ctx->L->stream));
     return GS_OK;
@@ -1029,7 +1035,16 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         return GS_OK;
     };
     switch (what) {
-    case GS_READ_KEYS: src = ctx->L->keys; avail = (size_t)ctx->E; break;
+    case GS_READ_KEYS:
+        if (!ctx->L->keys_sorted && ctx->stage >= 2) {  // the frame's entries again, sorted with their keys
+            gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals,
+                            (uint32_t)ctx->L->e_cap, nullptr, nullptr);
+            GS_HIP(ctx, hipGetLastError());
+            if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, ctx->E, ctx->err))
+                return set_error(ctx, rc, ctx->err);
+            ctx->L->keys_sorted = true;
+        }
+        src = ctx->L->keys; avail = (size_t)ctx->E; break;
     case GS_READ_VALS: src = ctx->L->vals; avail = (size_t)ctx->E; break;
     case GS_READ_BINS:
         if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");

@@ -74,9 +74,12 @@ struct SortScratch {
 // for).  With bins != null, also the reference's tile bins of the keys (countBins.glsl +
 // prefix: bins[t] = #keys with int(key) <= t) and the longest-first tile order in bins[256..511]
 // (what launch_bins computes), counted during the first pass's histogram read.
+// keys_out false (values < 2^24 required): only the values come out sorted -- the last two
+// passes move one packed word (top key byte | value) instead of the pair; keys is left holding
+// an intermediate order.
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
-               uint32_t *bins = nullptr);
+               uint32_t *bins = nullptr, bool keys_out = true);
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]

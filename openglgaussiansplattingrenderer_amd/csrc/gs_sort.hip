@@ -246,7 +246,13 @@ __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, 
     if (threadIdx.x == 0) row_total[blockIdx.x] = carry;
 }
 
-template <int W>
+// FMT: the pass's element format
+//   kPairs   (key, value) in, (key, value) out
+//   kPackOut (key, value) in, packed out: key's top byte | value (value < 2^24), into kout
+//   kPackIn  packed in (kin), value out (vout): the last pass of a frame sort, whose keys
+//            nobody reads (the draw needs the values and the bins only)
+constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2;
+template <int W, int FMT>
 __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     __shared__ int32_t s_gbase[kRadix];         // global position of local slot 0 of each digit
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_keys[kTile];
-    __shared__ uint32_t s_vals[kTile];
+    __shared__ uint32_t s_vals[FMT == kPackIn ? 1 : kTile];
 
     for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
@@ -275,14 +281,14 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
             kk[k] = pk[k * 64];
-            vv[k] = pv[k * 64];
+            vv[k] = FMT == kPackIn ? 0u : pv[k * 64];
         }
     } else {
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
             const uint32_t idx = base + k * 64;
             kk[k] = (idx < n) ? kin[idx] : 0u;
-            vv[k] = (idx < n) ? vin[idx] : 0u;
+            vv[k] = (FMT != kPackIn && idx < n) ? vin[idx] : 0u;
         }
     }
     // Stable rank of each key among this wave's keys of its digit, in (item, lane) order:
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
             const uint32_t d = (kk[k] >> shift) & 0xffu;
             const uint32_t pos = s_start[d] + s_cnt[wid][d] + rank[k];
             s_keys[pos] = kk[k];
-            s_vals[pos] = vv[k];
+            if (FMT != kPackIn) s_vals[pos] = vv[k];
         }
     }
     __syncthreads();
@@ -349,8 +355,14 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         const uint32_t key = s_keys[i];
         const uint32_t d = (key >> shift) & 0xffu;
         const uint32_t o = (uint32_t)(s_gbase[d] + (int32_t)i);
-        kout[o] = key;
-        vout[o] = s_vals[i];
+        if (FMT == kPairs) {
+            kout[o] = key;
+            vout[o] = s_vals[i];
+        } else if (FMT == kPackOut) {
+            kout[o] = (key & 0xff000000u) | s_vals[i];
+        } else {
+            vout[o] = key & 0x00ffffffu;
+        }
     }
 }
 
@@ -407,7 +419,7 @@ void sort_free(SortScratch &sc) {
 }
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
-               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins) {
+               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out) {
     if (((n <= 1 && !dev_count) || n < 1) && !bins) {  // nothing to sort; the events still mark the call
         if (start) (void)hipEventRecord(start, s);
         if (stop) (void)hipEventRecord(stop, s);
@@ -444,16 +456,25 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
                            dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
+        // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only
+        const int fmt = keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
         if (big)
-            hipExtLaunchKernelGGL(k_downsweep<kWaveBig>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin, vin,
-                                  kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+            hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
+                                  kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+        else if (fmt == kPairs)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
+                                  0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+        else if (fmt == kPackOut)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackOut>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         else
-            hipExtLaunchKernelGGL(k_downsweep<kWaveSmall>, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin,
-                                  vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackIn>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    // 4 (even) passes: the result is back in (keys, vals)
+    // 4 (even) passes: the result is back in (keys, vals); without keys_out, keys holds the
+    // pass-1 order
     if (hipGetLastError() != hipSuccess) {
         err = "radix sort: kernel launch failed";
         return GS_ERR_HIP;

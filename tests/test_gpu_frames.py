@@ -122,8 +122,9 @@ def near_camera_splats(ctx, W, H, n=20000, seed=5):
 
 
 def test_wide_key_range_sorts_all_bits(oracle):
-    """a frame whose keys span more than 2^27 bit patterns sorts all 32 bits (4 passes); the
-    3-pass sort of narrow frames is exercised by every other frame test"""
+    """a frame whose keys span more than 2^27 bit patterns (negative keys, all four digit
+    passes carrying information) sorts bit-exact; the frame sort leaves only the values
+    sorted, so reading the keys sorts the frame's entries again -- both must match the oracle"""
     W, H = 512, 384
     ctx = g.Context(0)
     sp = near_camera_splats(ctx, W, H)
@@ -140,8 +141,8 @@ def test_wide_key_range_sorts_all_bits(oracle):
 
 
 def test_wide_key_range_in_flight_renders_again():
-    """a frame enqueued without a round trip after narrow frames sorts in 3 passes; when its own
-    key range turns out wide it is detected at gs_sync and rendered again (4 passes)"""
+    """a frame with a wide key range enqueued without a round trip right after narrow frames,
+    and a narrow frame behind it: both images equal their host-synchronous renders"""
     W, H = 512, 384
     ctx = g.Context(0)
     means, rot, sc, op, col = c2_scene()
