@@ -94,7 +94,8 @@ void *gs_stream(gs_ctx *ctx);                /* the hipStream_t of the newest fr
                                                 (after gs_sync no other ctx stream has work) */
 /* Frames in flight on the device: 2 (default) -- consecutive frames alternate between two
  * streams with their own frame buffers, so frame k+1's preprocess, emission and sort overlap
- * frame k's blend (blends stay in frame order; everything else behaves as one stream) -- or 1.
+ * frame k's blend (blends into one output stay in frame order, blends into different outputs
+ * may overlap; everything else behaves as one stream) -- or 1.
  * Beyond the reference, whose gpuRender blocks per frame (src/Splats.cpp:580,595). */
 int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
 

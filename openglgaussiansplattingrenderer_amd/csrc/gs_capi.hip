@@ -51,9 +51,7 @@ struct Lane {
     // argsort key scratch
     uint32_t *ask = nullptr;
     size_t ask_cap = 0;
-    // ordering between lanes
-    hipEvent_t draw_done = nullptr;  // after this lane's newest blend
-    bool drew = false;
+    // ordering between lanes (blends: per frame slot, see enqueue_draw)
     hipEvent_t aux_done = nullptr;   // after this lane's newest non-frame work
     bool aux_pending = false;        // ... not yet waited for by the other lanes' frames
     hipEvent_t tail = nullptr;       // scratch: "all work so far" on this lane
@@ -88,6 +86,10 @@ struct gs_ctx {
         uint32_t flags = 0;
         void *out = nullptr;
         int64_t cap = 0;
+        // the frame's blend: lane, output and whether it writes the draw-stats buffer
+        int lane = -1;
+        const void *draw_out = nullptr;
+        bool drawn = false, draw_stats = false;
     };
     Slot slot[kRing];
     hipEvent_t ev[kRing][kEv] = {};
@@ -380,7 +382,6 @@ int gs_ctx_create(int device, gs_ctx **out) {
     if ((rc = use_device(ctx))) return fail(rc);
     for (Lane &ln : ctx->lane) {
         if (hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ln.draw_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ln.aux_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ln.tail, hipEventDisableTiming) != hipSuccess)
             return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
@@ -423,7 +424,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
-        for (hipEvent_t e : {ln.draw_done, ln.aux_done, ln.tail})
+        for (hipEvent_t e : {ln.aux_done, ln.tail})
             if (e) (void)hipEventDestroy(e);
         if (ln.stream) (void)hipStreamDestroy(ln.stream);
     }
@@ -863,16 +864,25 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.coverH = coverH;
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
-    // blends run in frame order: wait for the other lanes' newest blend
-    for (int i = 0; i < ctx->nlanes; ++i) {
-        Lane &o = ctx->lane[i];
-        if (&o != ctx->L && o.drew) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.draw_done, 0));
+    // Blends into one output land in frame order: wait for the frames in flight on other
+    // lanes that blend into the same output (or, with GS_FLAG_DRAW_STATS, into the shared
+    // stats buffer); frames into different outputs (a double-buffered texture) overlap.
+    // Retired slots are complete; a slot's last event rides on its draw kernel.
+    const bool with_stats = (flags & GS_FLAG_DRAW_STATS) != 0;
+    for (int i = 0; i < kRing; ++i) {
+        const gs_ctx::Slot &sl = ctx->slot[i];
+        if (i == ctx->cur || !sl.used || !sl.drawn || sl.lane == ctx->cur_lane) continue;
+        if (sl.draw_out == dst || (with_stats && sl.draw_stats))
+            GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->ev[i][kEv - 1], 0));
     }
     gs::launch_draw(ctx->L->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->L->bins, ctx->L->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
                     fev(ctx, 8));
     GS_HIP(ctx, hipGetLastError());
-    GS_HIP(ctx, hipEventRecord(ctx->L->draw_done, ctx->L->stream));
-    ctx->L->drew = true;
+    gs_ctx::Slot &me = ctx->slot[ctx->cur];
+    me.lane = ctx->cur_lane;
+    me.draw_out = dst;
+    me.drawn = true;
+    me.draw_stats = with_stats;
     if (!out_on_device) {
         GS_HIP(ctx, hipMemcpyAsync(out_rgba8, dst, npx * 4, hipMemcpyDeviceToHost, ctx->L->stream));
         GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));

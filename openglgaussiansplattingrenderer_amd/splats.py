@@ -524,12 +524,18 @@ class Splats:
         self.render_uniforms(u)
 
     def render_uniforms(self, u: N.gs_uniforms):
-        if u.width * u.height * 4 > self._texture.nbytes:
-            self._texture = DeviceBuffer(self.ctx, u.width * u.height * 4)
+        """One frame into the back texture, which then becomes the texture (double buffering: a
+        frame's blend need not wait for the previous frame's, gs_render orders blends per
+        output only)."""
+        nbytes = u.width * u.height * 4
+        back = getattr(self, "_back", None)
+        if back is None or nbytes > back.nbytes:
+            back = DeviceBuffer(self.ctx, max(nbytes, self._texture.nbytes))
         self.width, self.height = int(u.width), int(u.height)
         # no stats pointer: the frame is enqueued without a host round trip (gs_render)
-        check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, self._texture.ptr, 1, None),
+        check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, back.ptr, 1, None),
               self.ctx.handle)
+        self._back, self._texture = self._texture, back
 
     def saveImage(self, filename: str, flip_y: bool = False):
         """saveImage (src/Splats.cpp:516-540) of the current texture: RGBA PNG, row 0 = GL row 0

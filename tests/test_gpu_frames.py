@@ -219,3 +219,42 @@ def test_one_and_two_lanes_identical():
             ctx.set_lanes(3)
         finally:
             ctx.close()
+
+
+def test_rotating_outputs_keep_per_output_order():
+    """blends wait only for frames in flight into the same output: with three outputs rotated
+    over two lanes, frame k+3 (lane B) rewrites the output frame k (lane A) wrote -- each output
+    must end up holding the newest frame written into it"""
+    W, H = 384, 256
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    render_sync(sp, pose(W, H, 0), outs[0])
+    last = {}
+    for k in range(7):
+        render_spec(sp, pose(W, H, k), outs[k % 3])
+        last[k % 3] = k
+    ctx.sync()
+    got = [o.download(np.uint8, W * H * 4) for o in outs]
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    for i, k in last.items():
+        render_sync(sp, pose(W, H, k), ref)
+        assert np.array_equal(got[i], ref.download(np.uint8, W * H * 4)), f"output {i} (pose {k})"
+    ctx.close()
+
+
+def test_double_buffered_texture_is_newest_frame():
+    """Splats.render_uniforms renders into a back texture and swaps: texture() is the newest
+    frame's image"""
+    W, H = 384, 256
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    for k in range(5):
+        sp.render_uniforms(pose(W, H, k))
+    img = sp.texture().reshape(-1).copy()
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, pose(W, H, 4), ref)
+    assert np.array_equal(img, ref.download(np.uint8, W * H * 4))
+    ctx.close()
