@@ -174,9 +174,9 @@ def main():
     ap.add_argument("--fast-exp", action="store_true", help="GS_FLAG_FAST_EXP: hardware exp in the blend")
     ap.add_argument("--sh", action="store_true", help="GS_FLAG_SH: degree-3 SH colours (SURVEY f3, beyond the "
                     "reference; seeded synthetic f_rest)")
-    ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--lanes", type=int, default=3, choices=(1, 2, 3),
                     help="frames in flight per GPU (gs_ctx_set_lanes): 2 overlaps frame k+1's preprocess / "
-                         "emission / sort with frame k's blend")
+                         "emission / sort with frame k's blend, 3 (default here) also the blends' tails")
     ap.add_argument("--view", type=int, default=None,
                     help="C5 pose index to render (default: this rank's, main pose + rotateRight(45 deg * k))")
     ap.add_argument("--no-cpu-baseline", action="store_true")

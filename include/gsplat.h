@@ -92,7 +92,7 @@ void gs_ctx_destroy(gs_ctx *ctx);
 int gs_sync(gs_ctx *ctx);                    /* glFinish (src/Splats.cpp:595) */
 void *gs_stream(gs_ctx *ctx);                /* the hipStream_t of the newest frame, for interop
                                                 (after gs_sync no other ctx stream has work) */
-/* Frames in flight on the device: 2 (default) -- consecutive frames alternate between two
+/* Frames in flight on the device: 2 (default) or 3 -- consecutive frames rotate over that many
  * streams with their own frame buffers, so frame k+1's preprocess, emission and sort overlap
  * frame k's blend (blends into one output stay in frame order, blends into different outputs
  * may overlap; everything else behaves as one stream) -- or 1.

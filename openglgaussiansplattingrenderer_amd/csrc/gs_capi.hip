@@ -53,16 +53,16 @@ struct Lane {
     size_t ask_cap = 0;
     // ordering between lanes (blends: per frame slot, see enqueue_draw)
     hipEvent_t aux_done = nullptr;   // after this lane's newest non-frame work
-    bool aux_pending = false;        // ... not yet waited for by the other lanes' frames
+    uint32_t aux_waiters = 0;        // ... lanes (bits) whose next frame has yet to wait for it
     hipEvent_t tail = nullptr;       // scratch: "all work so far" on this lane
 };
-constexpr int kMaxLanes = 2;
+constexpr int kMaxLanes = 3;
 
 struct gs_ctx {
     int device = 0;
     std::string err;
     Lane lane[kMaxLanes];
-    int nlanes = kMaxLanes;  // frames in flight on the device (gs_ctx_set_lanes)
+    int nlanes = 2;  // frames in flight on the device (gs_ctx_set_lanes)
     int cur_lane = 0;
     Lane *L = &lane[0];      // the lane of the newest frame (and of non-frame work)
     unsigned long long *draw_stats = nullptr;  // GS_FLAG_DRAW_STATS trace (shared: blends are ordered)
@@ -160,10 +160,10 @@ int join_lanes(gs_ctx *ctx) {
     return GS_OK;
 }
 
-// ... and enqueued: the other lanes' next frames wait for it
+// ... and enqueued: each other lane's next frame waits for it
 int mark_aux(gs_ctx *ctx) {
     GS_HIP(ctx, hipEventRecord(ctx->L->aux_done, ctx->L->stream));
-    ctx->L->aux_pending = true;
+    ctx->L->aux_waiters = ((1u << ctx->nlanes) - 1) & ~(1u << ctx->cur_lane);
     return GS_OK;
 }
 
@@ -172,11 +172,12 @@ int mark_aux(gs_ctx *ctx) {
 int next_lane(gs_ctx *ctx) {
     ctx->cur_lane = (ctx->cur_lane + 1) % ctx->nlanes;
     ctx->L = &ctx->lane[ctx->cur_lane];
+    const uint32_t me = 1u << ctx->cur_lane;
     for (int i = 0; i < ctx->nlanes; ++i) {
         Lane &o = ctx->lane[i];
-        if (&o == ctx->L || !o.aux_pending) continue;
+        if (&o == ctx->L || !(o.aux_waiters & me)) continue;
         GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.aux_done, 0));
-        o.aux_pending = false;
+        o.aux_waiters &= ~me;
     }
     return GS_OK;
 }
@@ -442,8 +443,9 @@ void gs_ctx_destroy(gs_ctx *ctx) {
 // frame k's blend) or 1 (frames run one after the other on one stream)
 int gs_ctx_set_lanes(gs_ctx *ctx, int lanes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (lanes < 1 || lanes > kMaxLanes) return set_error(ctx, GS_ERR_INVALID, "gs_ctx_set_lanes: lanes must be 1 or 2");
+    if (lanes < 1 || lanes > kMaxLanes) return set_error(ctx, GS_ERR_INVALID, "gs_ctx_set_lanes: lanes must be 1, 2 or 3");
     if (int rc = gs_sync(ctx)) return rc;
+    for (Lane &ln : ctx->lane) ln.aux_waiters = 0;  // everything enqueued so far is done
     ctx->nlanes = lanes;
     ctx->cur_lane = std::min(ctx->cur_lane, lanes - 1);
     ctx->L = &ctx->lane[ctx->cur_lane];

@@ -49,7 +49,8 @@ class Context:
 
     def set_lanes(self, lanes: int):
         """frames in flight on the device (gs_ctx_set_lanes): 2 (default) overlaps frame k+1's
-        preprocess / emission / sort with frame k's blend; 1 runs frames one after the other"""
+        preprocess / emission / sort with frame k's blend; 3 keeps one more frame in flight
+        (throughput +1-2 % at C3); 1 runs frames one after the other"""
         check(lib().gs_ctx_set_lanes(self.handle, int(lanes)), self.handle)
 
     def timing_reset(self):
@@ -528,14 +529,18 @@ class Splats:
         frame's blend need not wait for the previous frame's, gs_render orders blends per
         output only)."""
         nbytes = u.width * u.height * 4
-        back = getattr(self, "_back", None)
+        backs = getattr(self, "_backs", None)
+        if backs is None:
+            backs = self._backs = [None, None]  # a ring of three textures (one per frame lane)
+        back = backs[0]  # the oldest texture
         if back is None or nbytes > back.nbytes:
             back = DeviceBuffer(self.ctx, max(nbytes, self._texture.nbytes))
         self.width, self.height = int(u.width), int(u.height)
         # no stats pointer: the frame is enqueued without a host round trip (gs_render)
         check(lib().gs_render(self.ctx.handle, self._scene, ctypes.byref(u), self.flags, back.ptr, 1, None),
               self.ctx.handle)
-        self._back, self._texture = self._texture, back
+        self._backs = backs[1:] + [self._texture]
+        self._texture = back
 
     def saveImage(self, filename: str, flip_y: bool = False):
         """saveImage (src/Splats.cpp:516-540) of the current texture: RGBA PNG, row 0 = GL row 0

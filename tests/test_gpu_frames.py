@@ -165,11 +165,13 @@ def test_wide_key_range_in_flight_renders_again():
     ctx.close()
 
 
-def test_two_lanes_keep_frame_order():
-    """consecutive frames alternate between two lanes (streams); blends into one output land in
-    frame order, and non-frame work between frames is ordered as on one stream"""
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_lanes_keep_frame_order(lanes):
+    """consecutive frames rotate over the lanes (streams); blends into one output land in frame
+    order, and non-frame work between frames is ordered as on one stream"""
     W, H = 384, 256
     ctx = g.Context(0)
+    ctx.set_lanes(lanes)
     means, rot, sc, op, col = c2_scene()
     sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
     out = g.DeviceBuffer(ctx, W * H * 4)
@@ -199,7 +201,7 @@ def test_two_lanes_keep_frame_order():
 def test_one_and_two_lanes_identical():
     W, H = 512, 384
     imgs = {}
-    for lanes in (1, 2):
+    for lanes in (1, 2, 3):
         ctx = g.Context(0)
         ctx.set_lanes(lanes)
         means, rot, sc, op, col = c2_scene()
@@ -211,12 +213,13 @@ def test_one_and_two_lanes_identical():
         ctx.sync()
         imgs[lanes] = [o.download(np.uint8, W * H * 4) for o in outs]
         ctx.close()
-    for a, b in zip(imgs[1], imgs[2]):
-        assert np.array_equal(a, b)
+    for lanes in (2, 3):
+        for a, b in zip(imgs[1], imgs[lanes]):
+            assert np.array_equal(a, b)
     with pytest.raises(g.GsError):
         ctx = g.Context(0)
         try:
-            ctx.set_lanes(3)
+            ctx.set_lanes(4)
         finally:
             ctx.close()
 
@@ -257,4 +260,27 @@ def test_double_buffered_texture_is_newest_frame():
     ref = g.DeviceBuffer(ctx, W * H * 4)
     render_sync(sp, pose(W, H, 4), ref)
     assert np.array_equal(img, ref.download(np.uint8, W * H * 4))
+    ctx.close()
+
+
+def test_memset_orders_before_every_lanes_next_frame():
+    """three lanes: a memset enqueued after frame A must precede the next frame of EACH other
+    lane -- here the second frame after it (on the third lane) rewrites the memset's target"""
+    W, H = 384, 256
+    ctx = g.Context(0)
+    ctx.set_lanes(3)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    out, other = g.DeviceBuffer(ctx, W * H * 4), g.DeviceBuffer(ctx, W * H * 4)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, pose(W, H, 2), ref)
+    want = ref.download(np.uint8, W * H * 4)
+    render_sync(sp, pose(W, H, 0), out)
+    for _ in range(3):
+        render_spec(sp, pose(W, H, 1), out)
+        check(lib().gs_memset(ctx.handle, out.ptr, 0, W * H * 4), ctx.handle)
+        render_spec(sp, pose(W, H, 1), other)  # next lane
+        render_spec(sp, pose(W, H, 2), out)    # the lane after: must blend after the memset
+        ctx.sync()
+        assert np.array_equal(out.download(np.uint8, W * H * 4), want)
     ctx.close()
