@@ -272,6 +272,12 @@ def main():
                                          (" (sharing the GPU with the next frame's stages)" if args.lanes > 1 else "")
                                          if dom == "draw" else "hipEvents of the stage-timing pass"),
                 "traffic": load_pmc(kern_name)}
+    if dom == "draw":  # the same kernel with the GPU to itself (the one-lane pass): its own roofline
+        one_ms = tm_serial["ms_draw"] / max(1, tm_serial["frames"])
+        one = alg["draw"] / (one_ms * 1e-3) / 1e9
+        roofline["one_frame"] = {"avg_launch_ms": round(one_ms, 4), "achieved": round(one, 2),
+                                 "frac": round(one / HBM_PEAK_GBS, 4),
+                                 "source": "hipEvents on the draw dispatch, frames one at a time (1 lane)"}
     frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
     frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
 

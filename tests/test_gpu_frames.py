@@ -132,10 +132,13 @@ def test_wide_key_range_sorts_all_bits(oracle):
     out = g.DeviceBuffer(ctx, W * H * 4)
     st = render_sync(sp, u, out)
     E = int(st.entries)
+    ref = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0, draw=False)
+    # the values as the frame's own sort left them (packed last passes, no keys) ...
+    assert np.array_equal(sp.read(g.GS_READ_VALS, E), ref["vals"])
+    # ... then the keys, which sorts the frame's entries again with keys, and the values again
     keys = sp.read(g.GS_READ_KEYS, E)
     vals = sp.read(g.GS_READ_VALS, E)
     assert int(keys.max()) - int(keys.min()) >= 1 << 27, "the case must be wide"
-    ref = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0, draw=False)
     assert np.array_equal(keys, ref["keys"]) and np.array_equal(vals, ref["vals"])
     ctx.close()
 

@@ -41,7 +41,10 @@ def gpu_frame(sp: g.Splats, u, flags):
     sp.flags = flags
     sp.render_uniforms(u)
     n, E = sp.numSplats, int(sp.stats.entries)
-    return dict(image=sp.texture(), keys=sp.read(g.GS_READ_KEYS, E), vals=sp.read(g.GS_READ_VALS, E),
+    # the values first, as the frame's sort left them (its last passes carry no keys); reading
+    # the keys then sorts the frame's entries again, with keys
+    vals = sp.read(g.GS_READ_VALS, E)
+    return dict(image=sp.texture(), keys=sp.read(g.GS_READ_KEYS, E), vals=vals,
                 bins=sp.read(g.GS_READ_BINS, 256), means2d=sp.read(g.GS_READ_MEANS2D, 2 * n, np.float32),
                 conics=sp.read(g.GS_READ_CONICS, 4 * n, np.float32), V=int(sp.stats.visible),
                 D=int(sp.stats.duplicates), E=E)
