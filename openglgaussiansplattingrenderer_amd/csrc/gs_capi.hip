@@ -547,6 +547,7 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
                     const float *colours4, gs_scene **out) {
     if (!ctx || !out || n < 0 || (n > 0 && (!means4 || !cov6 || !opacity || !colours4)))
         return set_error(ctx, GS_ERR_INVALID, "gs_scene_create: bad argument");
+    if (n > gs::kMaxSplats) return set_error(ctx, GS_ERR_INVALID, "gs_scene_create: more than 2^27 splats");
     *out = nullptr;
     if (int rc = use_device(ctx)) return rc;
     // host AoS (reference layout) -> device SoA planes
@@ -616,6 +617,10 @@ int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out) {
     int n = 0;
     std::FILE *f = nullptr;
     if (int rc = gs::ply_open_body(path, &n, &f)) return set_error(ctx, rc, gs_last_error(nullptr));
+    if (n > gs::kMaxSplats) {
+        std::fclose(f);
+        return set_error(ctx, GS_ERR_INVALID, "gs_scene_load_ply: more than 2^27 splats");
+    }
     const size_t nn = (size_t)n, rec = gs::kPlyFloats * sizeof(float);
     gs_scene *s = new gs_scene();
     s->ctx = ctx;

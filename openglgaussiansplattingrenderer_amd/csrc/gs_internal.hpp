@@ -31,6 +31,9 @@ int camera_uniforms(const gs_camera *cam, gs_uniforms *u);
 int save_png(const char *path, int width, int height, const uint8_t *rgba8, int flip_y);
 
 // ---------------------------------------------------------------- device side
+// splat ids address per-splat records through 32-bit byte offsets (32-B blend records: the
+// blend's gathers), so a scene holds at most 2^27 splats (bicycle: 6.1M)
+constexpr int kMaxSplats = 1 << 27;
 constexpr int kTiles = 16;  // the reference's fixed 16x16 coarse grid (preprocess.glsl:143-153)
 
 // Per-frame uniforms of the preprocess kernel (preprocess.glsl:18-37)

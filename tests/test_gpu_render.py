@@ -161,3 +161,15 @@ def test_stage_order_errors():
     assert g.lib().gs_sort(c.handle) == GS_ERR_STATE
     assert g.lib().gs_compute_bins(c.handle) == GS_ERR_STATE
     c.close()
+
+
+def test_scene_size_limit(ctx):
+    """scenes hold at most 2^27 splats (32-bit byte offsets into the 32-B blend records): more is
+    refused before any array is read"""
+    import ctypes
+    from openglgaussiansplattingrenderer_amd import _native as N
+    a = np.zeros(16, np.float32)
+    h = ctypes.c_void_p()
+    rc = N.lib().gs_scene_create(ctx.handle, (1 << 27) + 1, N.ptr(a), N.ptr(a), N.ptr(a), N.ptr(a), ctypes.byref(h))
+    assert rc < 0 and not h.value
+    assert b"2^27" in N.lib().gs_last_error(ctx.handle)
