@@ -191,7 +191,13 @@ def main():
     W, H = cfg["W"], cfg["H"]
     flags = ((g.GS_FLAG_CLEAN if args.clean else 0) | (g.GS_FLAG_FAST_EXP if args.fast_exp else 0) |
              (g.GS_FLAG_SH if args.sh else 0))
-    ctx = g.Context(local)
+    # one GPU per rank; ranks beyond the node's GPUs share them round-robin (labelled below)
+    import ctypes
+    from openglgaussiansplattingrenderer_amd import _native as native
+    ndev = ctypes.c_int(0)
+    native.lib().gs_device_count(ctypes.byref(ndev))
+    ndev = max(1, ndev.value)
+    ctx = g.Context(local % ndev)
     ctx.set_lanes(args.lanes)
     sp, data_desc = load_scene(args.config, W, H, ctx, flags)
     if args.sh:
@@ -307,7 +313,8 @@ def main():
                        (", fast exp" if args.fast_exp else ", defined exp") +
                        (", SH degree 3 (beyond the reference)" if args.sh else ""),
                        "splats": N, "width": W, "height": H, "views_per_gpu": 1,
-                       "parallelism": f"replicas x{world} (independent views, no collective); "
+                       "parallelism": f"replicas x{world} (independent views, no collective"
+                                      + (f"; {world} ranks on {ndev} GPU(s)" if world > ndev else "") + "); "
                                       f"{args.lanes} frame(s) in flight per GPU"},
             "frame": {"V": V, "D": D, "E": E, "D_over_N": round(D / max(N, 1), 4),
                       "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
