@@ -287,3 +287,44 @@ def test_memset_orders_before_every_lanes_next_frame():
         ctx.sync()
         assert np.array_equal(out.download(np.uint8, W * H * 4), want)
     ctx.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_random_frame_sequences_keep_per_output_order(seed):
+    """random mixes of frames without a round trip, host-synchronous frames, memsets and lane
+    changes over four outputs: each output ends up holding the newest thing written into it
+    (the image of the last frame into it, or zeros after a memset)"""
+    W, H = 256, 192
+    rng = np.random.default_rng(seed)
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(4)]
+    render_sync(sp, pose(W, H, 0), outs[0])
+    last = {}  # output -> pose, or None for zeros
+    for _ in range(80):
+        r = rng.random()
+        o = int(rng.integers(0, 4))
+        if r < 0.6:
+            k = int(rng.integers(0, 7))
+            render_spec(sp, pose(W, H, k), outs[o])
+            last[o] = k
+        elif r < 0.75:
+            k = int(rng.integers(0, 7))
+            render_sync(sp, pose(W, H, k), outs[o])
+            last[o] = k
+        elif r < 0.9:
+            check(lib().gs_memset(ctx.handle, outs[o].ptr, 0, W * H * 4), ctx.handle)
+            last[o] = None
+        else:
+            ctx.set_lanes(int(rng.integers(1, 4)))
+    ctx.sync()
+    got = [b.download(np.uint8, W * H * 4) for b in outs]
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    for o, k in last.items():
+        if k is None:
+            assert not got[o].any(), f"output {o}: memset expected"
+        else:
+            render_sync(sp, pose(W, H, k), ref)
+            assert np.array_equal(got[o], ref.download(np.uint8, W * H * 4)), f"output {o}: pose {k}"
+    ctx.close()
