@@ -289,8 +289,8 @@ def test_memset_orders_before_every_lanes_next_frame():
     ctx.close()
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3, 4])
-def test_random_frame_sequences_keep_per_output_order(seed):
+@pytest.mark.parametrize("seed,flags", [(1, 0), (2, 0), (3, g.GS_FLAG_CLEAN), (4, g.GS_FLAG_FAST_EXP)])
+def test_random_frame_sequences_keep_per_output_order(seed, flags):
     """random mixes of frames without a round trip, host-synchronous frames, memsets and lane
     changes over four outputs: each output ends up holding the newest thing written into it
     (the image of the last frame into it, or zeros after a memset)"""
@@ -298,7 +298,7 @@ def test_random_frame_sequences_keep_per_output_order(seed):
     rng = np.random.default_rng(seed)
     ctx = g.Context(0)
     means, rot, sc, op, col = c2_scene()
-    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx, flags=flags)
     outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(4)]
     render_sync(sp, pose(W, H, 0), outs[0])
     last = {}  # output -> pose, or None for zeros
