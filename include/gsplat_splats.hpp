@@ -47,7 +47,8 @@ class Context {
     gs_ctx *get() const { return ctx_; }
     void finish() const { report(gs_sync(ctx_), ctx_); }  // glFinish
     // frames in flight on the device: 2 (default; frame k+1's preprocess / emission / sort
-    // overlap frame k's blend) or 1 (one frame at a time, as gpuRender blocks)
+    // overlap frame k's blend), 3 (one more in flight), or 1 (one frame at a time, as
+    // gpuRender blocks)
     int setLanes(int lanes) const { return report(gs_ctx_set_lanes(ctx_, lanes), ctx_); }
 
   private:
