@@ -848,7 +848,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         if (cull && keep)  // uniform
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
-        while (keep && !all_done) {
+        // one exit (a uniform loop condition, no continue / return inside): fewer scalar
+        // control-flow instructions per survivor
+        bool turned = false;
+        while (keep && !all_done && !turned) {
             const int src = __builtin_ctzll(keep);
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
@@ -883,7 +886,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
             }
-            if (nev == 0) continue;  // uniform
+            if (nev != 0) {  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
             // v_mbcnt); each pixel occurs at most once, so the events are independent.  Every
             // lane writes each slot: lanes without that event into their own spare entry.
@@ -933,8 +936,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             // every lane runs an event (no exec mask around it): lanes >= nev repeat the last
             // one, reading the same old state and writing the same new state to one address
             event(min((uint32_t)lane, nev - 1u));
-            if (nev > 64)  // uniform, rare: more events than lanes
-                for (uint32_t e = lane + 64; e < nev; e += 64) event(e);
+            // rare: more events than lanes -- uniform passes, lanes past the end repeat the
+            // pass's last event (which no earlier pass held)
+            for (uint32_t e0p = 64; e0p < nev; e0p += 64) event(min(e0p + (uint32_t)lane, nev - 1u));
             if (ballot(sat >= __float_as_uint(0.99f))) {  // uniform, rare: a pixel saturated -- refresh the done masks
                 wave_lds_sync();
                 D0 = ballot(s_col[4 * lane + 0].w >= 0.99f);
@@ -942,14 +946,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 D2 = ballot(s_col[4 * lane + 2].w >= 0.99f);
                 D3 = ballot(s_col[4 * lane + 3].w >= 0.99f);
                 all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
-                if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) {
-                    wave_lds_sync();
-                    return true;
-                }
+                turned = !all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64;
             }
             wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
+            }
         }
-        return false;
+        return turned;
     };
 
     // sparse phase (see go_sparse): one pixel per lane, state in registers
@@ -979,20 +981,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 st_pxneed += __popcll(nb);
                 st_ev64 += __popcll(nb);
             }
-            if (!nb) continue;  // uniform
-            const float o = rl(d.o, src);
-            const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
-            const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
-            const float alpha = fminf(0.99f, ex * o);
-            const bool take = ((nb >> lane) & 1) & !(alpha < 1.0f / 255.0f);
-            // alphaBlend :59-67
-            const float aT = alpha * (1.0f - pc.w);
-            pc.x = take ? pc.x + r * aT : pc.x;
-            pc.y = take ? pc.y + g * aT : pc.y;
-            pc.z = take ? pc.z + bl * aT : pc.z;
-            pc.w = take ? pc.w + aT : pc.w;
-            SA &= ~ballot(pc.w >= 0.99f);  // :129-133
-            all_done = SA == 0;
+            if (nb) {  // uniform (no continue: one loop exit)
+                const float o = rl(d.o, src);
+                const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
+                const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
+                const float alpha = fminf(0.99f, ex * o);
+                const bool take = ((nb >> lane) & 1) & !(alpha < 1.0f / 255.0f);
+                // alphaBlend :59-67
+                const float aT = alpha * (1.0f - pc.w);
+                pc.x = take ? pc.x + r * aT : pc.x;
+                pc.y = take ? pc.y + g * aT : pc.y;
+                pc.z = take ? pc.z + bl * aT : pc.z;
+                pc.w = take ? pc.w + aT : pc.w;
+                SA &= ~ballot(pc.w >= 0.99f);  // :129-133
+                all_done = SA == 0;
+            }
         }
         if ((uint32_t)lane < nact) s_col[spix] = pc;  // distinct pixels
         wave_lds_sync();
