@@ -850,8 +850,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         if (STATS) st_surv += __popcll(keep);
         // one exit (a uniform loop condition, no continue / return inside): fewer scalar
         // control-flow instructions per survivor
-        bool turned = false;
-        while (keep && !all_done && !turned) {
+        bool turned = false, stop = all_done;  // stop = all_done | turned, set only on a refresh
+        while (keep && !stop) {
             const int src = __builtin_ctzll(keep);
             keep &= keep - 1;
             const float mx = rl(d.mx, src), my = rl(d.my, src);
@@ -947,6 +947,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 D3 = ballot(s_col[4 * lane + 3].w >= 0.99f);
                 all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
                 turned = !all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64;
+                stop = all_done | turned;
             }
             wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
             }
