@@ -761,6 +761,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     bool sparse = false;
     uint64_t SA = 0;   // lanes whose pixel is active
     uint32_t spix = 0, nact = 0;
+    float4 pc = make_float4(0.f, 0.f, 0.f, 0.f);  // the lane's pixel state in the sparse phase
     auto go_sparse = [&]() {
         wave_lds_sync();
         const uint64_t A0 = ~D0, A1 = ~D1, A2 = ~D2, A3 = ~D3;
@@ -795,6 +796,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         irx1 = (uint32_t)((int)rx1 + kBoxBias);
         iry0 = (uint32_t)((int)ry0 + kBoxBias);
         iry1 = (uint32_t)((int)ry1 + kBoxBias);
+        pc = s_col[spix];  // stays in registers to the end (written back once)
         sparse = true;
     };
     // blocks with few pixels in the image start sparse
@@ -961,7 +963,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         if (!keep) return;  // uniform
-        float4 pc = s_col[spix];
         const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
         const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
         while (keep && !all_done) {
@@ -998,8 +999,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 all_done = SA == 0;
             }
         }
-        if ((uint32_t)lane < nact) s_col[spix] = pc;  // distinct pixels
-        wave_lds_sync();
     };
 
     // prologue: chunk 0 box-gathered, chunk 1 index-loaded ... see the stage table above
@@ -1036,6 +1035,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             if (!step(std::integral_constant<int, 1>{})) break;
         }
     }
+    if (sparse && (uint32_t)lane < nact) s_col[spix] = pc;  // the sparse phase's state (distinct pixels)
     wave_lds_sync();
     if (in00) out[(size_t)pya * P.W + pxa] = pack_rgba8(s_col[4 * lane + 0]);
     if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 1]);
