@@ -188,106 +188,101 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         const float c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
         const float c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
         const float opac = sc.opacity[i];
-        float2 m2 = make_float2(0.f, 0.f);
-        float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 box = make_float4(__builtin_inff(), -__builtin_inff(), __builtin_inff(), -__builtin_inff());
-        int4 rc = make_int4(0, -1, -1, 0);
-        float lg = 0.0f;  // ln(255 o) for the culling quantities below (hardware log, see there)
-        do {
-            // :77-78
-            float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
-            float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
-            float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
-            const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
-            const float w = fmaxf(p3, 0.0001f);
-            p0 = p0 / w;
-            p1 = p1 / w;
-            p2 = p2 / w;
-            // :80-89 cull: NDC x/y only
-            if (p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f) break;
-            // :91-94
-            float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
-            const float sz = (p2 + 1.0f) * 0.5f;
-            sx = sx * (float)P.W;
-            sy = sy * (float)P.H;
-            if (P.clean && !(sz >= 0.0f && sz <= 1.0f)) break;  // clean: near/far cull (Q6)
-            m2 = make_float2(sx, sy);
-            // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
-            const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
-            const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
-                            {P.view[8], P.view[9], P.view[10]}}};
-            // :110-116
-            float tx = m4v_row(P.view, 0, mx, my, mz, 1.0f);
-            float ty = m4v_row(P.view, 1, mx, my, mz, 1.0f);
-            const float tz = m4v_row(P.view, 2, mx, my, mz, 1.0f);
-            const float limx = -1.3f * P.tan_fov_x, limy = -1.3f * P.tan_fov_y;
-            const float txtz = tx / tz, tytz = ty / tz;
-            tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
-            ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
-            // :118-128
-            const M3 J = {{{P.fx / tz, 0.0f, -(P.fx * tx) / (tz * tz)},
-                           {0.0f, P.fy / tz, -(P.fy * ty) / (tz * tz)},
-                           {0.0f, 0.0f, 0.0f}}};
-            const M3 T = mul3(tr3(W3), J);
-            M3 C = mul3(mul3(tr3(T), tr3(Sig)), T);
-            C.v[0][0] += 0.3f;
-            C.v[1][1] += 0.3f;
-            // :129-136
-            const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
-            const float det = ca * cc - cb * cb;
-            if (det == 0) break;                   // Q7: entry omitted
-            if (P.clean && !(det > 0.0f)) break;
-            const float inv = 1.0f / det;
-            co = make_float4(cc * inv, -cb * inv, ca * inv, opac);
-            // :139-149
-            const float middle = (cc + ca) * 0.5f;
-            const float l1 = middle + sqrtf(fmaxf(0.1f, middle * middle - det));
-            const float l2 = middle - sqrtf(fmaxf(0.1f, middle * middle - det));
-            const float radius = ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
-            const int minX = max(0, f2i((sx - radius) / P.tile_w));
-            const int maxX = min(15, f2i((sx + radius) / P.tile_w));
-            const int minY = max(0, f2i((sy - radius) / P.tile_h));
-            const int maxY = min(15, f2i((sy + radius) / P.tile_h));
-            // :151-155 main tile (unclamped in ref mode, Q5)
-            int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
-            if (P.clean) {
-                tileX = min(15, max(0, tileX));
-                tileY = min(15, max(0, tileY));
-            }
-            const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
-            const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
-            n_main += 1;
-            n_dup += (uint32_t)(rectCount - mainInRect);
-            const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
-                                ((uint32_t)maxY << 24);
-            rc = make_int4((int)f2u(sz), tileX, tileY, (int)rp);
+        // Straight-line body: every cull folds into `vis` and the outputs are selected at the
+        // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
+        // all ten plane loads issue up front and no exec-mask bookkeeping runs).  Culled lanes
+        // compute garbage (inf / NaN) that is never used.
+        // :77-78
+        float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
+        float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
+        float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
+        const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
+        const float w = fmaxf(p3, 0.0001f);
+        p0 = p0 / w;
+        p1 = p1 / w;
+        p2 = p2 / w;
+        // :80-89 cull: NDC x/y only
+        bool vis = !(p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f);
+        // :91-94
+        float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
+        const float sz = (p2 + 1.0f) * 0.5f;
+        sx = sx * (float)P.W;
+        sy = sy * (float)P.H;
+        if (P.clean) vis = vis && (sz >= 0.0f && sz <= 1.0f);  // clean: near/far cull (Q6)
+        // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
+        const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
+        const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
+                        {P.view[8], P.view[9], P.view[10]}}};
+        // :110-116
+        float tx = m4v_row(P.view, 0, mx, my, mz, 1.0f);
+        float ty = m4v_row(P.view, 1, mx, my, mz, 1.0f);
+        const float tz = m4v_row(P.view, 2, mx, my, mz, 1.0f);
+        const float limx = -1.3f * P.tan_fov_x, limy = -1.3f * P.tan_fov_y;
+        const float txtz = tx / tz, tytz = ty / tz;
+        tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+        ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
+        // :118-128
+        const M3 J = {{{P.fx / tz, 0.0f, -(P.fx * tx) / (tz * tz)},
+                       {0.0f, P.fy / tz, -(P.fy * ty) / (tz * tz)},
+                       {0.0f, 0.0f, 0.0f}}};
+        const M3 T = mul3(tr3(W3), J);
+        M3 C = mul3(mul3(tr3(T), tr3(Sig)), T);
+        C.v[0][0] += 0.3f;
+        C.v[1][1] += 0.3f;
+        // :129-136
+        const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
+        const float det = ca * cc - cb * cb;
+        vis = vis && det != 0;  // Q7: entry omitted
+        if (P.clean) vis = vis && det > 0.0f;
+        const float inv = 1.0f / det;
+        const float4 cov2 = make_float4(cc * inv, -cb * inv, ca * inv, opac);
+        // :139-149
+        const float middle = (cc + ca) * 0.5f;
+        const float l1 = middle + sqrtf(fmaxf(0.1f, middle * middle - det));
+        const float l2 = middle - sqrtf(fmaxf(0.1f, middle * middle - det));
+        const float radius = ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+        const int minX = max(0, f2i((sx - radius) / P.tile_w));
+        const int maxX = min(15, f2i((sx + radius) / P.tile_w));
+        const int minY = max(0, f2i((sy - radius) / P.tile_h));
+        const int maxY = min(15, f2i((sy + radius) / P.tile_h));
+        // :151-155 main tile (unclamped in ref mode, Q5)
+        int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
+        if (P.clean) {
+            tileX = min(15, max(0, tileX));
+            tileY = min(15, max(0, tileY));
+        }
+        const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+        const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
+        n_main += vis ? 1u : 0u;
+        n_dup += vis ? (uint32_t)(rectCount - mainInRect) : 0u;
+        const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
+                            ((uint32_t)maxY << 24);
 
-            // Conservative pixel box of the region where alpha >= 1/255 can hold
-            // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
-            // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
-            // culling an entry outside the box never changes a pixel.
-            // The box and the pre-exp threshold only cull (they never enter a pixel's
-            // arithmetic) and carry margins far above hardware-instruction error (0.05 in ln,
-            // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
-            // v_sqrt instead of the correctly rounded library sequences.
-            const float A = co.x, B = co.y, Cq = co.z;
-            lg = __logf(255.0f * opac);
-            const float tau = lg + 0.05f;
-            if (!(tau > 0.0f)) {
-                // never reaches 1/255 anywhere: empty box (stays +inf,-inf)
-            } else {
-                const float detQ = A * Cq - B * B;
-                const float trq = A + Cq;
-                if (A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ) {
-                    const float rq = __builtin_amdgcn_rcpf(detQ);
-                    const float hx = __builtin_amdgcn_sqrtf(2.0f * tau * Cq * rq) * 1.02f + 1.0f;
-                    const float hy = __builtin_amdgcn_sqrtf(2.0f * tau * A * rq) * 1.02f + 1.0f;
-                    box = make_float4(sx - hx, sx + hx, sy - hy, sy + hy);
-                } else {
-                    box = make_float4(-__builtin_inff(), __builtin_inff(), -__builtin_inff(), __builtin_inff());
-                }
-            }
-        } while (false);
+        // Conservative pixel box of the region where alpha >= 1/255 can hold
+        // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
+        // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
+        // culling an entry outside the box never changes a pixel.
+        // The box and the pre-exp threshold only cull (they never enter a pixel's
+        // arithmetic) and carry margins far above hardware-instruction error (0.05 in ln,
+        // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
+        // v_sqrt instead of the correctly rounded library sequences.
+        const float A = cov2.x, B = cov2.y, Cq = cov2.z;
+        const float lg = __logf(255.0f * opac);  // ln(255 o)
+        const float tau = lg + 0.05f;
+        const float detQ = A * Cq - B * B;
+        const float trq = A + Cq;
+        const bool wellc = A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ;
+        const float rq = __builtin_amdgcn_rcpf(detQ);
+        const float hx = __builtin_amdgcn_sqrtf(2.0f * tau * Cq * rq) * 1.02f + 1.0f;
+        const float hy = __builtin_amdgcn_sqrtf(2.0f * tau * A * rq) * 1.02f + 1.0f;
+        const float inf = __builtin_inff();
+        // tau <= 0: never reaches 1/255 anywhere (empty box); ill-conditioned: unbounded box
+        const float4 box = !(tau > 0.0f) ? make_float4(inf, -inf, inf, -inf)
+                           : wellc       ? make_float4(sx - hx, sx + hx, sy - hy, sy + hy)
+                                         : make_float4(-inf, inf, -inf, inf);
+        const float2 m2 = make_float2(sx, sy);
+        const float4 co = cov2;
+        const int4 rc = vis ? make_int4((int)f2u(sz), tileX, tileY, (int)rp) : make_int4(0, -1, -1, 0);
         // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
         // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
         // becomes -inf, which never skips
