@@ -451,7 +451,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             uint32_t *kd = keys + d0;
             uint32_t *vd = vals + d0;
             const int ibase = blockIdx.x * kSplatsPerBlock + it * kBlock + wid * 64;
-            for (uint32_t e = lane; e < T; e += 64) {
+            const uint32_t lim = min(T, room);  // entries to write
+            // uniform trip count (lanes past the end compute a harmless owner, store nothing)
+            for (uint32_t e0 = 0; e0 < T; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
                 int s = 0;  // owner: first lane with incl > e
 #pragma unroll
                 for (int step = 32; step > 0; step >>= 1)
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
                 const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
                 const uint32_t dy = k / (uint32_t)w, dx = k - dy * (uint32_t)w;
                 const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
-                if (e < room) {
+                if (e < lim) {
                     kd[e] = f2u((float)tile + u2f((uint32_t)r.x));
                     vd[e] = (uint32_t)(ibase + s);
                 }
