@@ -126,7 +126,7 @@ __host__ __device__ constexpr uint32_t xcd_grid(uint32_t nb) { return 8 * ((nb +
 // digits leave short runs per tile, so a larger tile doubles the scatter's write runs)
 // tile_counts != null: also countBins.glsl:20-31 -- tile_counts[int(key)] += 1 for int(key) in
 // [0, 256), LDS replicas, then one global atomic per nonzero tile and workgroup
-template <int W>
+template <int W, bool TILES>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
@@ -139,8 +139,11 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
-    __shared__ uint32_t s_tiles[kRadix * kRep];
-    for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) s_cnt[i] = s_tiles[i] = 0;
+    __shared__ uint32_t s_tiles[TILES ? kRadix * kRep : 1];
+    for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) {
+        s_cnt[i] = 0;
+        if (TILES) s_tiles[i] = 0;
+    }
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         const uint32_t idx = base + k * 64;
         if (idx < n) {
             atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
-            if (tile_counts) {  // uniform
+            if (TILES) {  // the frame's tile counts ride on the first pass
                 const uint32_t t = (uint32_t)f2i(__uint_as_float(kk[k]));
                 if (t < (uint32_t)kRadix) atomicAdd(&s_tiles[t * kRep + rep], 1u);
             }
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         return (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
     };
     hist[(size_t)d * nb + tile] = sum8(&s_cnt[d * kRep]);
-    if (tile_counts) {
+    if (TILES) {
         const uint32_t c = sum8(&s_tiles[d * kRep]);
         if (c) atomicAdd(&tile_counts[(blockIdx.x % kTileCopies) * kRadix + d], c);
     }
@@ -447,12 +450,15 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
-        if (big)
-            hipExtLaunchKernelGGL(k_upsweep<kWaveBig>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin,
-                                  (uint32_t)n, dev_count, shift, sc.hist, nb, bins ? tile_counts : nullptr);
+        if (big && bins)
+            hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
+                                  kin, (uint32_t)n, dev_count, shift, sc.hist, nb, tile_counts);
+        else if (big)
+            hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
+                                  kin, (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
         else
-            hipExtLaunchKernelGGL(k_upsweep<kWaveSmall>, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin,
-                                  (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
+            hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
+                                  0, kin, (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
         const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
                            dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
