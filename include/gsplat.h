@@ -187,12 +187,15 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
             float tile_h, uint32_t flags, void *out_rgba8, int out_on_device);
 
 /* frame-state readback for parity tests (host buffers; counts in elements) */
-#define GS_READ_KEYS 1      /* uint32[E] sorted (after gs_sort) or emitted key bits */
+#define GS_READ_KEYS 1      /* uint32[E] sorted (after gs_sort / gs_render) or emitted key bits;
+                               gs_render's own sort carries no keys through its last passes,
+                               so this read emits and sorts that frame's entries again */
 #define GS_READ_VALS 2      /* uint32[E] splat index per entry */
 #define GS_READ_BINS 3      /* uint32[256] inclusive tile ends (after gs_compute_bins) */
 #define GS_READ_MEANS2D 4   /* float[2N] */
 #define GS_READ_CONICS 5    /* float[4N] conic.xyz + opacity */
-#define GS_READ_CULLBOX 6   /* float[4N] per-splat pixel box used by the block cull */
+#define GS_READ_CULLBOX 6   /* float[4N] per-splat pixel box used by the block cull (whole pixels:
+                               the device keeps floor/ceil 16-bit bounds) */
 int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count);
 
 /* ------------------------------------------------------------- radix sort */
