@@ -35,6 +35,37 @@ CONFIGS = {
 }
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their environment, 127.0.0.1 rendezvous) and wait for them.  The
+    parent never touches the GPU (no HIP call before the children exist); rank 0 prints the
+    JSON line.  A failing rank ends the others (they would wait at a barrier)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for q in live:  # the exact children we started
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -182,9 +213,34 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (spawn / rendezvous / per-rank pose / barrier / gather), no GPU: "
+                         "prints a dry-run line, not a measurement (tests/test_dist_cpu.py)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, local, pg = dist_setup()
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting {world} rank(s)", file=sys.stderr)
+    if args.dry_run:
+        if os.environ.get("GS_BENCH_DRYRUN_FAIL_RANK") == str(rank):  # tests: a rank that dies
+            sys.exit(3)
+        view = rank if args.view is None else args.view
+        cfg = CONFIGS[args.config]
+        u = camera_for_rank(cfg["W"], cfg["H"], view).uniforms()
+        barrier(pg)
+        mine = {"rank": rank, "local_rank": local, "view": view, "view_matrix": [round(x, 6) for x in u.view]}
+        ranks = [mine]
+        if pg is not None:
+            ranks = [None] * world
+            pg.all_gather_object(ranks, mine)
+        mx = max_over_ranks(pg, float(rank + 1))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "max_over_ranks": mx, "ranks": ranks}), flush=True)
+        if pg is not None:
+            pg.destroy_process_group()
+        return
     import openglgaussiansplattingrenderer_amd as g
 
     cfg = CONFIGS[args.config]
@@ -208,43 +264,53 @@ def main():
     view = rank if args.view is None else args.view
     u = camera_for_rank(W, H, view).uniforms()
 
+    # one frame at a time (gs_ctx_set_lanes 1), measured before the timed region: the frame
+    # latency, then the per-stage breakdown (the same frames with every stage boundary timed,
+    # stages not sharing the GPU with the next frame's)
+    nser = max(5, min(args.steps, 50))
+    ctx.set_lanes(1)
+    for _ in range(2):
+        sp.render_uniforms(u)
+    ctx.sync()
+    ctx.timing_enable(g.GS_TIMING_DRAW)
+    ctx.timing_reset()
+    ts0 = time.perf_counter()
+    for _ in range(nser):
+        sp.render_uniforms(u)
+    ctx.sync()
+    serial_ms = (time.perf_counter() - ts0) / nser * 1e3
+    tm_serial = ctx.timing_read()
+    ctx.timing_enable(g.GS_TIMING_STAGES)
+    ctx.timing_reset()
+    for _ in range(nser):
+        sp.render_uniforms(u)
+    tm = ctx.timing_read()
+
+    # the timed region: W warmup frames, then exactly K frames between barriers and device
+    # syncs, on args.lanes frames in flight; every frame carries only its draw kernel's
+    # start/stop events (each hipEvent idles the stream a few microseconds)
+    ctx.set_lanes(args.lanes)
+    ctx.timing_enable(g.GS_TIMING_DRAW)
     for _ in range(args.warmup):
         sp.render_uniforms(u)
     ctx.sync()
-    # timed region: every frame carries only its draw kernel's start/stop events (each hipEvent
-    # idles the stream a few microseconds, so per-stage events are kept out of this loop)
-    ctx.timing_enable(g.GS_TIMING_DRAW)
     barrier(pg)
     ctx.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sp.render_uniforms(u)
+    t_enq = time.perf_counter()
     ctx.sync()
     t1 = time.perf_counter()
     barrier(pg)
     local_s = t1 - t0
     elapsed = max_over_ranks(pg, local_s)
     tm_draw = ctx.timing_read()
-    # one frame at a time (gs_ctx_set_lanes 1): the frame latency, and the per-stage breakdown
-    # (the same frames again with every stage boundary timed, stages not sharing the GPU with
-    # the next frame's)
-    ctx.set_lanes(1)
-    for _ in range(2):
-        sp.render_uniforms(u)
-    ctx.sync()
-    ctx.timing_reset()
-    ts0 = time.perf_counter()
-    for _ in range(args.steps):
-        sp.render_uniforms(u)
-    ctx.sync()
-    serial_ms = (time.perf_counter() - ts0) / args.steps * 1e3
-    tm_serial = ctx.timing_read()
-    ctx.timing_enable(g.GS_TIMING_STAGES)
-    ctx.timing_reset()
-    for _ in range(args.steps):
-        sp.render_uniforms(u)
-    tm = ctx.timing_read()
-    ctx.set_lanes(args.lanes)
+    host = {"enqueue_ms_per_frame": round((tm_draw["ms_host_render"] - tm_draw["ms_host_wait"]) /
+                                          max(1, tm_draw["host_renders"]), 4),
+            "blocked_ms_per_frame": round(tm_draw["ms_host_wait"] / max(1, tm_draw["host_renders"]), 4),
+            "python_loop_ms_per_frame": round((t_enq - t0) / args.steps * 1e3, 4),
+            "source": "host wall time inside gs_render (libgsplat_hip), minus its waits on frames in flight"}
     st = sp.stats
     N, V, D, E = int(st.num_splats), int(st.visible), int(st.duplicates), int(st.entries)
     frames_total = world * args.steps
@@ -287,6 +353,13 @@ def main():
     frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
     frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
 
+    # per-rank (view, entries, time) to rank 0 (gloo, host side)
+    mine = {"rank": rank, "device": local % ndev, "view": view, "E": E, "ms_per_frame": round(local_s / args.steps * 1e3, 4)}
+    ranks = [mine]
+    if pg is not None:
+        ranks = [None] * world
+        pg.all_gather_object(ranks, mine)
+
     sort = None
     if not args.no_sort_bench and rank == 0:
         sort = sort_bench(ctx)
@@ -318,11 +391,13 @@ def main():
                                       f"{args.lanes} frame(s) in flight per GPU"},
             "frame": {"V": V, "D": D, "E": E, "D_over_N": round(D / max(N, 1), 4),
                       "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-                      "stage_ms_source": "the same frames one at a time (1 lane) with every stage boundary timed",
+                      "stage_ms_source": f"{nser} frames one at a time (1 lane) with every stage boundary timed, before the timed region",
                       "frames_in_flight": args.lanes,
                       "serial_ms_per_frame": round(serial_ms, 4),
                       "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
                       "frame_hbm_frac_algorithmic": round(frame_frac, 4)},
+            "host": host,
+            "ranks": ranks,
             "roofline": roofline,
             "sort": sort,
             "cpu_baseline": cpu,

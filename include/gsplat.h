@@ -223,6 +223,10 @@ typedef struct gs_timing {
     double ms_bins;        /* tile bins */
     double ms_draw;        /* blend */
     double ms_frame;       /* first to last event of the frame (includes the E readback gap) */
+    double ms_host_render; /* host wall time inside gs_render calls */
+    double ms_host_wait;   /* ... of it blocked on frames in flight (slot reuse, readbacks):
+                              ms_host_render - ms_host_wait is the host's enqueue cost */
+    int64_t host_renders;  /* gs_render calls timed */
 } gs_timing;
 int gs_timing_reset(gs_ctx *ctx);
 /* which hipEvents a frame records (each event idles the stream a few microseconds):

@@ -88,6 +88,9 @@ class gs_timing(ctypes.Structure):
         ("ms_bins", ctypes.c_double),
         ("ms_draw", ctypes.c_double),
         ("ms_frame", ctypes.c_double),
+        ("ms_host_render", ctypes.c_double),
+        ("ms_host_wait", ctypes.c_double),
+        ("host_renders", ctypes.c_int64),
     ]
 
 

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -104,6 +105,7 @@ struct gs_ctx {
     std::vector<gs_scene *> scenes;  // live scenes (detached when the ctx goes first)
     bool e_known = false;        // an entry count has been observed (sizes speculative frames)
     gs_timing acc = {};
+    bool in_render = false;      // inside gs_render: host waits count as ms_host_wait
 };
 
 struct gs_scene {
@@ -142,16 +144,17 @@ int use_device(gs_ctx *ctx) {
     return GS_OK;
 }
 
-// wait on the host for every lane
+// wait on the host for every lane (all of them: after gs_ctx_set_lanes lowered the count, the
+// newest frame and its non-frame work may sit on a lane beyond it)
 int sync_lanes(gs_ctx *ctx) {
-    for (int i = 0; i < ctx->nlanes; ++i) GS_HIP(ctx, hipStreamSynchronize(ctx->lane[i].stream));
+    for (Lane &ln : ctx->lane) GS_HIP(ctx, hipStreamSynchronize(ln.stream));
     return GS_OK;
 }
 
 // non-frame work about to be enqueued on the current lane: order it after everything enqueued
 // so far on the other lanes (on the device), as a single stream would
 int join_lanes(gs_ctx *ctx) {
-    for (int i = 0; i < ctx->nlanes; ++i) {
+    for (int i = 0; i < kMaxLanes; ++i) {
         Lane &o = ctx->lane[i];
         if (&o == ctx->L) continue;
         GS_HIP(ctx, hipEventRecord(o.tail, o.stream));
@@ -163,7 +166,7 @@ int join_lanes(gs_ctx *ctx) {
 // ... and enqueued: each other lane's next frame waits for it
 int mark_aux(gs_ctx *ctx) {
     GS_HIP(ctx, hipEventRecord(ctx->L->aux_done, ctx->L->stream));
-    ctx->L->aux_waiters = ((1u << ctx->nlanes) - 1) & ~(1u << ctx->cur_lane);
+    ctx->L->aux_waiters = ((1u << kMaxLanes) - 1) & ~(1u << ctx->cur_lane);
     return GS_OK;
 }
 
@@ -173,7 +176,7 @@ int next_lane(gs_ctx *ctx) {
     ctx->cur_lane = (ctx->cur_lane + 1) % ctx->nlanes;
     ctx->L = &ctx->lane[ctx->cur_lane];
     const uint32_t me = 1u << ctx->cur_lane;
-    for (int i = 0; i < ctx->nlanes; ++i) {
+    for (int i = 0; i < kMaxLanes; ++i) {
         Lane &o = ctx->lane[i];
         if (&o == ctx->L || !(o.aux_waiters & me)) continue;
         GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, o.aux_done, 0));
@@ -306,7 +309,12 @@ int handle_overflow(gs_ctx *ctx) {
 int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
     for (int k; (k = oldest_used(ctx, seq_limit)) >= 0;) {
         gs_ctx::Slot &sl = ctx->slot[k];
-        GS_HIP(ctx, hipEventSynchronize(ctx->ev[k][kEv - 1]));
+        {
+            const auto w0 = std::chrono::steady_clock::now();
+            GS_HIP(ctx, hipEventSynchronize(ctx->ev[k][kEv - 1]));
+            if (ctx->in_render)
+                ctx->acc.ms_host_wait += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        }
         if (sl.spec) {
             const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
             if (V + D > sl.cap) return handle_overflow(ctx);
@@ -333,6 +341,18 @@ int validate_all(gs_ctx *ctx) {
     if (!any_spec(ctx)) return GS_OK;
     if (int rc = sync_lanes(ctx)) return rc;
     return retire_upto(ctx, ~0ull);
+}
+
+// Before a new frame picks its lane and sizes that lane's buffers: retire the frame holding the
+// slot it will take.  Retiring may find an overflowed speculative frame and render it again
+// (handle_overflow -> render_sync), which moves ctx->L and ctx->cur; after this loop
+// begin_frame retires nothing, so the lane and buffers chosen next stay the frame's own.
+int prepare_frame(gs_ctx *ctx) {
+    for (;;) {
+        const gs_ctx::Slot &sl = ctx->slot[(ctx->cur + 1) % kRing];
+        if (!sl.used) return GS_OK;
+        if (int rc = retire_upto(ctx, sl.seq)) return rc;
+    }
 }
 
 // take the next slot for a new frame (retiring the frame that held it)
@@ -446,9 +466,9 @@ int gs_ctx_set_lanes(gs_ctx *ctx, int lanes) {
     if (lanes < 1 || lanes > kMaxLanes) return set_error(ctx, GS_ERR_INVALID, "gs_ctx_set_lanes: lanes must be 1, 2 or 3");
     if (int rc = gs_sync(ctx)) return rc;
     for (Lane &ln : ctx->lane) ln.aux_waiters = 0;  // everything enqueued so far is done
+    // L stays on the newest frame's lane (gs_frame_read / gs_draw / gs_sort still address that
+    // frame's buffers); next_lane takes the new count from the next frame on
     ctx->nlanes = lanes;
-    ctx->cur_lane = std::min(ctx->cur_lane, lanes - 1);
-    ctx->L = &ctx->lane[ctx->cur_lane];
     return GS_OK;
 }
 
@@ -475,6 +495,8 @@ int gs_free(gs_ctx *ctx, void *dptr) {
 }
 int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    // an overflowed speculative frame is rendered again before this write, not over it
+    if (int rc = validate_all(ctx)) return rc;
     if (int rc = join_lanes(ctx)) return rc;  // frames in flight may read dst
     GS_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->L->stream));
     GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));
@@ -489,6 +511,7 @@ int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes) {
 }
 int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (int rc = validate_all(ctx)) return rc;  // see gs_memcpy_h2d
     if (int rc = join_lanes(ctx)) return rc;
     GS_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->L->stream));
     return mark_aux(ctx);
@@ -913,6 +936,7 @@ int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
 // the device and are sized by the entry capacity (last observed count + 25 % + 64Ki); the
 // slot keeps what is needed to render the frame again should the count exceed it.
 int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out) {
+    if (int rc = prepare_frame(ctx)) return rc;
     if (int rc = next_lane(ctx)) return rc;
     const int64_t want = std::max<int64_t>(ctx->E + ctx->E / 4 + 65536, (int64_t)scene->n + 4096);
     if (ctx->L->e_cap < want)
@@ -943,6 +967,7 @@ extern "C" {
 int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, gs_frame_stats *stats) {
     if (int rc = check_frame_args(ctx, scene, u, "gs_preprocess")) return rc;
     if (int rc = validate_all(ctx)) return rc;
+    if (int rc = prepare_frame(ctx)) return rc;
     if (int rc = next_lane(ctx)) return rc;  // a new frame
     if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
     // E is needed on the host to size the sort (the reference maps its atomic counter back
@@ -996,10 +1021,30 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     return enqueue_draw(ctx, scene, width, height, tile_w, tile_h, flags, out_rgba8, out_on_device, ctx->E, nullptr);
 }
 
+namespace {
+int render_impl(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
+                int out_on_device, gs_frame_stats *stats);
+}
+
 int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
               int out_on_device, gs_frame_stats *stats) {
     if (!out_rgba8) return set_error(ctx, GS_ERR_INVALID, "gs_render: null argument");
     if (int rc = check_frame_args(ctx, scene, u, "gs_render")) return rc;
+    // host cost of the call (enqueue vs blocked on frames in flight), gs_timing_read
+    const auto t0 = std::chrono::steady_clock::now();
+    ctx->in_render = true;
+    const int rc = render_impl(ctx, scene, u, flags, out_rgba8, out_on_device, stats);
+    ctx->in_render = false;
+    ctx->acc.ms_host_render += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    ctx->acc.host_renders += 1;
+    return rc;
+}
+
+}  // extern "C"
+
+namespace {
+int render_impl(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out_rgba8,
+                int out_on_device, gs_frame_stats *stats) {
     // no stats wanted, output on the device, an entry count seen before: enqueue the whole
     // frame without a host round trip (validated at gs_sync / the next readback)
     if (!stats && out_on_device && ctx->e_known && !(flags & GS_FLAG_TIMING))
@@ -1018,6 +1063,9 @@ int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t
     }
     return GS_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats) {
     if (!ctx || !stats) return set_error(ctx, GS_ERR_INVALID, "gs_last_stats: null argument");
@@ -1126,6 +1174,7 @@ int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n
     if (!ctx || (n > 0 && (!d_keys || !d_order)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_argsort_f32: bad argument");
     if (n <= 1) return GS_OK;
     if (int rc = use_device(ctx)) return rc;
+    if (int rc = validate_all(ctx)) return rc;  // see gs_memcpy_h2d (the outputs may alias a frame's)
     if ((size_t)n > ctx->L->ask_cap) {
         if (int rc = grow(ctx, ctx->L->ask, (size_t)n + (size_t)n / 4)) return rc;
         ctx->L->ask_cap = (size_t)n + (size_t)n / 4;
@@ -1141,6 +1190,7 @@ int gs_argsort_f32(gs_ctx *ctx, const float *d_keys, int32_t *d_order, int64_t n
 int gs_sort_pairs_u32(gs_ctx *ctx, uint32_t *d_keys, uint32_t *d_vals, int64_t n) {
     if (!ctx || (n > 0 && (!d_keys || !d_vals)) || n < 0) return set_error(ctx, GS_ERR_INVALID, "gs_sort_pairs_u32: bad argument");
     if (int rc = use_device(ctx)) return rc;
+    if (int rc = validate_all(ctx)) return rc;  // see gs_memcpy_h2d
     if (int rc = join_lanes(ctx)) return rc;
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, d_keys, d_vals, n, ctx->err, nullptr, ctx->evs[0], ctx->evs[1]))
         return set_error(ctx, rc, ctx->err);

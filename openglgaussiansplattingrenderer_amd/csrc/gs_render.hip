@@ -313,7 +313,8 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
     }
     // block sums of (main, dup) for the emission offsets
     uint32_t tot_main, tot_dup;
-    {  // one scan of both: mains in the low 11 bits (<= 1024 per block), duplicates above (<= 261120)
+    {  // one scan of both: mains in the low 11 bits (<= 1024 per block), duplicates above (<= 256
+       // per splat, main tile outside the rect included: <= 262144 per block, 21 bits)
         uint32_t tot;
         block_excl_scan256(n_main | (n_dup << 11), s_wave, &tot);
         tot_main = tot & 0x7ffu;
@@ -425,10 +426,12 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             n_main = 1;
             n_dup = (uint32_t)(rectCount - mainInRect);
         }
-        // one scan of both: mains in the low 16 bits (<= 256 per item), duplicates above (<= 65280)
+        // one scan of both: mains in the low 9 bits (<= 256 per item), duplicates above (<= 256
+        // per splat -- a main tile outside its rect, Q5, leaves the whole rect as duplicates --
+        // so <= 65536 per item, 23 bits)
         uint32_t tp;
-        const uint32_t pp = block_excl_scan256(n_main | (n_dup << 16), s_wave, &tp);
-        const uint32_t pm = pp & 0xffffu, pd = pp >> 16, t0 = tp & 0xffffu, t1 = tp >> 16;
+        const uint32_t pp = block_excl_scan256(n_main | (n_dup << 9), s_wave, &tp);
+        const uint32_t pm = pp & 0x1ffu, pd = pp >> 9, t0 = tp & 0x1ffu, t1 = tp >> 9;
         if (has) {
             // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
             const uint32_t mpos = carry_m + pm;

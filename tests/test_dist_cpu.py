@@ -55,3 +55,35 @@ def test_single_rank_defaults(monkeypatch):
     w, r, local, pg = bench.dist_setup()
     assert (w, r, local, pg) == (1, 0, 0, None)
     assert bench.max_over_ranks(None, 3.5) == 3.5
+
+
+def test_gpus_flag_spawns_ranks():
+    """`bench.py --gpus N` with no launcher environment starts N rank processes itself (the
+    parent makes no GPU call); rank 0 prints one line with every rank's view (dry run: the
+    plumbing only, no GPU)"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["dry_run"] and d["n_gpus"] == 3 and d["max_over_ranks"] == 3.0
+    assert [x["rank"] for x in d["ranks"]] == [0, 1, 2] and [x["view"] for x in d["ranks"]] == [0, 1, 2]
+    assert len({tuple(x["view_matrix"]) for x in d["ranks"]}) == 3  # each rank its own pose
+
+
+def test_failing_rank_ends_the_spawn():
+    """a rank that fails makes `bench.py --gpus N` exit non-zero (the others are ended)"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    env["GS_BENCH_DRYRUN_FAIL_RANK"] = "1"  # rank 1 exits before the rendezvous; rank 0 would wait
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3

@@ -328,3 +328,112 @@ def test_random_frame_sequences_keep_per_output_order(seed, flags):
             render_sync(sp, pose(W, H, k), ref)
             assert np.array_equal(got[o], ref.download(np.uint8, W * H * 4)), f"output {o}: pose {k}"
     ctx.close()
+
+
+def test_overflow_retired_by_a_larger_scenes_frame():
+    """a frame without a round trip that overflowed is retired (and rendered again,
+    which moves the ctx to other lanes) by the begin of a later frame of a LARGER scene: that
+    frame must size the buffers of the lane it finally runs on -- every image equals its
+    host-synchronous render"""
+    W, H = 640, 480
+    ctx = g.Context(0)
+    small = make_splats(ctx, 500, 1, W, H)
+    big = make_splats(ctx, 200_000, 2, W, H)
+    huge = make_splats(ctx, 400_000, 3, W, H)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(6)]
+    u = pose(W, H, 0)
+    render_sync(small, u, outs[0])              # capacity sized for ~500 splats
+    seq = [(big, 1), (small, 2), (small, 3), (small, 4), (huge, 5)]
+    for sp, o in seq:                           # big overflows; huge's frame retires it (ring of 4)
+        render_spec(sp, u, outs[o])
+    ctx.sync()
+    got = [b.download(np.uint8, W * H * 4) for b in outs]
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    for sp, o in seq:
+        render_sync(sp, u, ref)
+        assert np.array_equal(got[o], ref.download(np.uint8, W * H * 4)), f"output {o}"
+    ctx.close()
+
+
+@pytest.mark.parametrize("write", ["memset", "upload"])
+def test_overflow_then_write_keeps_the_write(write):
+    """an overflowed frame is rendered again BEFORE a later memset / upload into its
+    output, so the output holds what was written last"""
+    W, H = 640, 480
+    ctx = g.Context(0)
+    small = make_splats(ctx, 500, 1, W, H)
+    big = make_splats(ctx, 200_000, 2, W, H)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    u = pose(W, H, 0)
+    render_sync(small, u, out)
+    render_spec(big, u, out)                    # overflows (detected at the next validation)
+    pattern = (np.arange(W * H * 4) % 251).astype(np.uint8)
+    if write == "memset":
+        check(lib().gs_memset(ctx.handle, out.ptr, 0, W * H * 4), ctx.handle)
+        want = np.zeros(W * H * 4, np.uint8)
+    else:
+        out.upload(pattern)
+        want = pattern
+    ctx.sync()
+    assert np.array_equal(out.download(np.uint8, W * H * 4), want)
+    ctx.close()
+
+
+@pytest.mark.parametrize("frames", [1, 2, 3, 4])
+def test_set_lanes_keeps_newest_frame_readable(frames):
+    """lowering the lane count after frames on three lanes leaves the newest frame's
+    buffers addressed (reads return that frame's entries, not another lane's)"""
+    W, H = 384, 256
+    ctx = g.Context(0)
+    ctx.set_lanes(3)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    for k in range(frames):
+        st = render_sync(sp, pose(W, H, k), out)
+    E = int(st.entries)
+    vals = sp.read(g.GS_READ_VALS, E)
+    keys = sp.read(g.GS_READ_KEYS, E)
+    ctx.set_lanes(1)
+    assert np.array_equal(sp.read(g.GS_READ_VALS, E), vals)
+    assert np.array_equal(sp.read(g.GS_READ_KEYS, E), keys)
+    # and the next frames run on the new lane count
+    render_spec(sp, pose(W, H, 5), out)
+    ctx.sync()
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, pose(W, H, 5), ref)
+    assert np.array_equal(out.download(np.uint8, W * H * 4), ref.download(np.uint8, W * H * 4))
+    ctx.close()
+
+
+def test_emission_full_batch_of_out_of_rect_mains(oracle):
+    """at a width not divisible by 16 (ref mode, Q5) a splat right of column 16*int(W/16)
+    has its main tile outside its clamped rect, so ALL rect tiles are duplicates (256 for a
+    splat covering the grid); 256 of them in one emission batch give 65536 duplicates -- the
+    emission's packed block scan must not wrap"""
+    W, H = 1000, 600
+    ctx = g.Context(0)
+    u = g.main_camera(W, H).uniforms()
+    VP = np.array(u.vp[:], np.float64).reshape(4, 4).T
+    n = 1024
+    rng = np.random.default_rng(11)
+    sx = rng.uniform(993.0, 999.0, n)                       # int(W/16) = 62: tileX = 16
+    sy = rng.uniform(20.0, 580.0, n)
+    ndc = np.stack([2 * sx / W - 1, 2 * sy / H - 1, np.full(n, 0.5), np.ones(n)], 1)
+    wpt = (np.linalg.inv(VP) @ ndc.T).T
+    means = (wpt[:, :3] / wpt[:, 3:]).astype(np.float32)
+    rot = np.tile(np.array([1, 0, 0, 0], np.float32), (n, 1))
+    log_sc = np.full((n, 3), np.log(3.0), np.float32)       # covers the whole grid
+    op = np.full(n, -3.0, np.float32)                        # sigmoid: ~0.047 (slow saturation)
+    col = rng.normal(size=(n, 3)).astype(np.float32)
+    sp = g.Splats.from_raw(means, col, op, log_sc, rot, W, H, ctx=ctx)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    st = render_sync(sp, u, out)
+    ref = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0)
+    assert int(st.duplicates) >= 256 * 256, "the case must fill a batch with 256-duplicate splats"
+    assert int(st.entries) == ref["E"]
+    E = int(st.entries)
+    assert np.array_equal(sp.read(g.GS_READ_VALS, E), ref["vals"])
+    assert np.array_equal(sp.read(g.GS_READ_KEYS, E), ref["keys"])
+    assert np.array_equal(out.download(np.uint8, W * H * 4), ref["image"].reshape(-1))
+    ctx.close()
