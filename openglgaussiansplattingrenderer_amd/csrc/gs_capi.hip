@@ -41,11 +41,12 @@ struct Lane {
     // entries
     int64_t e_cap = 0;
     uint32_t *keys = nullptr, *vals = nullptr;
+    uint32_t *vals_base = nullptr;  // the allocation: kValsPad zero words, then vals (k_draw reads vals[-1] = 0)
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     gs::SortScratch sort;
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
-    uint32_t *bins = nullptr;        // [256] tile ranges + [256] draw dispatch order
+    uint32_t *bins = nullptr;        // [256] tile ranges + [256] draw dispatch order + keys above 1e6 (kBinsWords)
     // output staging (host-destination renders)
     uint32_t *img = nullptr;
     size_t img_cap = 0;
@@ -212,7 +213,11 @@ int ensure_entries(gs_ctx *ctx, int64_t e) {
     if (e <= ctx->L->e_cap) return GS_OK;
     const int64_t cap = e + e / 4 + 4096;
     int rc;
-    if ((rc = grow(ctx, ctx->L->keys, (size_t)cap)) || (rc = grow(ctx, ctx->L->vals, (size_t)cap))) return rc;
+    if ((rc = grow(ctx, ctx->L->keys, (size_t)cap)) || (rc = grow(ctx, ctx->L->vals_base, (size_t)cap + gs::kValsPad)))
+        return rc;
+    // the words before vals stay zero (nothing writes them): splat 0 for k_draw's culled entries
+    GS_HIP(ctx, hipMemset(ctx->L->vals_base, 0, gs::kValsPad * 4));
+    ctx->L->vals = ctx->L->vals_base + gs::kValsPad;
     ctx->L->e_cap = cap;
     return GS_OK;
 }
@@ -406,10 +411,10 @@ int gs_ctx_create(int device, gs_ctx **out) {
             hipEventCreateWithFlags(&ln.aux_done, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ln.tail, hipEventDisableTiming) != hipSuccess)
             return fail(set_error(nullptr, GS_ERR_HIP, "hipStreamCreate / hipEventCreate failed"));
-        if (hipMalloc(&ln.totals, 16) != hipSuccess || hipMalloc(&ln.bin_counts, 256 * 4) != hipSuccess ||
-            hipMalloc(&ln.bins, 512 * 4) != hipSuccess)
+        if (hipMalloc(&ln.totals, 16) != hipSuccess || hipMalloc(&ln.bin_counts, gs::kBinCountWords * 4) != hipSuccess ||
+            hipMalloc(&ln.bins, gs::kBinsWords * 4) != hipSuccess)
             return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
-        if (hipMemset(ln.bin_counts, 0, 256 * 4) != hipSuccess)
+        if (hipMemset(ln.bin_counts, 0, gs::kBinCountWords * 4) != hipSuccess)
             return fail(set_error(nullptr, GS_ERR_HIP, "ctx setup failed"));
     }
     if (hipHostMalloc(&ctx->h_ring, 16 * kRing, hipHostMallocDefault) != hipSuccess ||
@@ -440,7 +445,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
         if (ln.stream) (void)hipStreamSynchronize(ln.stream);
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
-        void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals,
+        void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
                         ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
@@ -892,6 +897,8 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     }
     P.coverW = coverW;
     P.coverH = coverH;
+    P.n = scene->n;
+    P.V = (int32_t)ctx->V;  // used when count is null (the frame's counts are on the host)
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other

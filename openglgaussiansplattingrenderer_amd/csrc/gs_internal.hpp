@@ -35,6 +35,13 @@ int save_png(const char *path, int width, int height, const uint8_t *rgba8, int 
 // blend's gathers), so a scene holds at most 2^27 splats (bicycle: 6.1M)
 constexpr int kMaxSplats = 1 << 27;
 constexpr int kTiles = 16;  // the reference's fixed 16x16 coarse grid (preprocess.glsl:143-153)
+// preprocess.glsl:83 depth of a culled splat (1e6f), as key bits.  The reference leaves culled
+// splats in the sorted range (as splat 0, splatKeys = 0): after every key whose bits are <= these
+// (k_draw places them virtually; bins[512] = the number of entries with larger key bits)
+constexpr uint32_t kKeyCulledBits = 0x49742400u;
+constexpr int kValsPad = 16;         // zero words before a frame's sorted values (vals[-1] = splat 0)
+constexpr int kBinsWords = 520;      // bins buffer: [256] tile ends, [256] draw order, [512] keys above 1e6
+constexpr int kBinCountWords = 260;  // counts of k_bins_count: [0, 256) tiles, [256] keys above 1e6
 
 // Per-frame uniforms of the preprocess kernel (preprocess.glsl:18-37)
 struct PreParams {
@@ -58,6 +65,8 @@ struct DrawParams {
     int32_t no_cull;
     int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
     int32_t coverW, coverH;     // drawn coverage; pixels outside it are zeroed (Q9)
+    int32_t n;                  // splats of the scene
+    int32_t V;                  // splats with entries (when count is null; else count[0])
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };

@@ -287,7 +287,10 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
         // becomes -inf, which never skips
         // the blend record, box and (GS_FLAG_SH) colour are read only through entries: written
-        // for the splats that have some (gs_frame_read shows the others as culled)
+        // for the splats that have some (gs_frame_read shows the others as culled), and for
+        // splat 0, which the reference's culled entries draw (preprocess.glsl:80-88 splatKeys = 0,
+        // reached by a Q10 over-read; k_draw): without entries its record is the culled one --
+        // means2D, conic and opacity 0 (never blends: threshold +inf, empty box)
         if (rc.y >= 0) {
         float thr = -lg - 1.0e-3f;
         if (thr != thr) thr = -__builtin_inff();
@@ -303,6 +306,10 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             fr.col[i] = make_float4(sh_channel(sc.sh, n, i, 0, dx, dy, dz), sh_channel(sc.sh, n, i, 1, dx, dy, dz),
                                     sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
         }
+        }
+        else if (i == 0) {  // splat 0 culled: the record its culled entries draw
+            fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, __builtin_inff(), 0.0f};
+            fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
         }
         if (PACK)
             reinterpret_cast<uint2 *>(fr.rec)[i] =
@@ -493,11 +500,13 @@ __global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restric
                                                        uint32_t *__restrict__ counts) {
     const int64_t E = cnt ? min(E_max, (int64_t)cnt[0] + (int64_t)cnt[1]) : E_max;
     __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_above;
     s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_above = 0;
     __syncthreads();
     const int64_t base = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kBinItems;
     int cur = -1;
-    uint32_t run = 0;
+    uint32_t run = 0, above = 0;
     if (base < E) {
         uint32_t kk[kBinItems];
         if (base + kBinItems <= E) {
@@ -516,6 +525,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restric
         }
 #pragma unroll
         for (int q = 0; q < kBinItems; ++q) {
+            above += (kk[q] > kKeyCulledBits && base + q < E) ? 1u : 0u;
             const int v = f2i(u2f(kk[q]));
             if (v < 0 || v >= 256) continue;
             if (v == cur) {
@@ -527,10 +537,12 @@ __global__ __launch_bounds__(kBlock) void k_bins_count(const uint32_t *__restric
             }
         }
         if (run) atomicAdd(&s_cnt[cur], run);
+        if (above) atomicAdd(&s_above, above);
     }
     __syncthreads();
     const uint32_t c = s_cnt[threadIdx.x];
     if (c) atomicAdd(&counts[threadIdx.x], c);
+    if (threadIdx.x == 0 && s_above) atomicAdd(&counts[256], s_above);
 }
 
 // prefixBins.glsl: inclusive scan of the 256 counts
@@ -543,6 +555,10 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(uint32_t *__restrict__ cou
     const uint32_t v = counts[threadIdx.x];
     counts[threadIdx.x] = 0;  // ready for the next frame's k_bins_count (no memset launch)
     s_cnt[threadIdx.x] = v;
+    if (threadIdx.x == 0) {  // keys above 1e6 (bits): where the reference's culled entries sit (k_draw)
+        bins[512] = counts[256];
+        counts[256] = 0;
+    }
     uint32_t tot;
     const uint32_t ex = block_excl_scan256(v, s_wave, &tot);  // (contains __syncthreads)
     bins[threadIdx.x] = ex + v;
@@ -712,11 +728,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 
     const int start = (t == 0) ? 0 : (int)bins[t - 1];
     int end = (int)bins[t];
+    // Positions are the reference's (ref mode): its sorted range also holds one entry per culled
+    // splat, key 1e6, drawn as splat 0 (preprocess.glsl:80-88, draw.glsl:97-98), after every key
+    // whose bits are <= 1e6's.  They are never binned, so only a Q10 window reaches them; here
+    // they are virtual: positions [cpos, cpos + cn) read splat 0, later ones entry p - cn.
+    // (uniform: pinned to scalar registers -- in VGPRs they were spilled, and the reload inside
+    // the list loop waited for every gather in flight)
+    const int E = __builtin_amdgcn_readfirstlane(P.count ? min(P.E, (int)(P.count[0] + P.count[1])) : P.E);
+    const int cn = __builtin_amdgcn_readfirstlane(P.clean ? 0 : max(0, P.n - (P.count ? (int)P.count[0] : P.V)));
+    const int cpos = __builtin_amdgcn_readfirstlane(min(max(E - (int)bins[2 * kTiles * kTiles], 0), E));
     if (!P.clean && end > start) {  // Q10: the last 1024-entry chunk is blended whole
-        const int E = P.count ? min(P.E, (int)(P.count[0] + P.count[1])) : P.E;
         const int chunks = (end - start + 1023) / 1024;
-        end = min(E, start + chunks * 1024);
+        end = min(E + cn, start + chunks * 1024);
     }
+    const int qmax = max(E - 1, 0);
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
 #pragma unroll
@@ -824,7 +849,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     auto at = [](const auto *base, uint32_t byte_off) {
         return reinterpret_cast<decltype(base)>(reinterpret_cast<const char *>(base) + byte_off);
     };
-    auto load_idx = [&](int base, uint32_t &v) { v = *at(vals, (uint32_t)min(base + lane, jmax) << 2); };
+    // position p -> word of vals - 1 (the word before vals is 0: a culled entry, splat 0)
+    const uint32_t *vals_m1 = vals - 1;
+    auto load_idx = [&](int base, uint32_t &v) {
+        const int p = min(base + lane, jmax);
+        const int q = p < cpos ? p : p < cpos + cn ? -1 : p - cn;
+        v = *at(vals_m1, (uint32_t)(min(q, qmax) + 1) << 2);
+    };
     auto gather_box = [&](uint32_t v, uint32_t &vb, uint2 &bx) {
         vb = v;
         bx = *at(cullbox, v << 3);
@@ -1038,10 +1069,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     }
     if (sparse && (uint32_t)lane < nact) s_col[spix] = pc;  // the sparse phase's state (distinct pixels)
     wave_lds_sync();
-    if (in00) out[(size_t)pya * P.W + pxa] = pack_rgba8(s_col[4 * lane + 0]);
-    if (in10) out[(size_t)pya * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 1]);
-    if (in01) out[(size_t)(pya + 1) * P.W + pxa] = pack_rgba8(s_col[4 * lane + 2]);
-    if (in11) out[(size_t)(pya + 1) * P.W + pxa + 1] = pack_rgba8(s_col[4 * lane + 3]);
+    {  // the quad's pixels again from the lane id (v_mbcnt, which the compiler does not merge with
+       // the kernel's start): nothing of the pixel layout stays live across the list loop (it was
+       // spilled there, a private segment in the dominant kernel)
+        const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int qx = x0 + 2 * (l2 & 7), qy = y0 + 2 * (l2 >> 3);
+        uint32_t *row0 = out + (size_t)qy * P.W + qx, *row1 = row0 + P.W;
+        if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[4 * l2 + 0]);
+        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[4 * l2 + 1]);
+        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[4 * l2 + 2]);
+        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[4 * l2 + 3]);
+    }
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         if (L < kDrawTraceBlocks) {

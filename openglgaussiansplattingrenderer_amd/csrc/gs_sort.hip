@@ -140,10 +140,12 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
     __shared__ uint32_t s_cnt[kRadix * kRep];
     __shared__ uint32_t s_tiles[TILES ? kRadix * kRep : 1];
+    __shared__ uint32_t s_above;
     for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) {
         s_cnt[i] = 0;
         if (TILES) s_tiles[i] = 0;
     }
+    if (TILES && threadIdx.x == 0) s_above = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
@@ -160,6 +162,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         }
     }
     const uint32_t rep = (uint32_t)lane & (kRep - 1);
+    uint32_t above = 0;
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
@@ -168,10 +171,16 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
             if (TILES) {  // the frame's tile counts ride on the first pass
                 const uint32_t t = (uint32_t)f2i(__uint_as_float(kk[k]));
                 if (t < (uint32_t)kRadix) atomicAdd(&s_tiles[t * kRep + rep], 1u);
+                above += kk[k] > kKeyCulledBits ? 1u : 0u;  // entries after the reference's culled ones
             }
         }
     }
+    if (TILES) {
+        above = wave_incl_scan(above);
+        if (lane == 63 && above) atomicAdd(&s_above, above);
+    }
     __syncthreads();
+    if (TILES && threadIdx.x == 0 && s_above) atomicAdd(&tile_counts[kTileCopies * kRadix + (blockIdx.x % kTileCopies)], s_above);
     const int d = threadIdx.x;
     if (d >= kRadix) return;
     auto sum8 = [](const uint32_t *p) {
@@ -199,6 +208,14 @@ __device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ 
         counts[k * kRadix + t] = 0;
     }
     s_c[t] = v;
+    if (t < kTileCopies) {  // entries with key bits above 1e6 (k_draw places the culled ones before them)
+        const uint32_t a = counts[kTileCopies * kRadix + t];
+        counts[kTileCopies * kRadix + t] = 0;
+        uint32_t sa = a;
+#pragma unroll
+        for (int o = 1; o < kTileCopies; o <<= 1) sa += __shfl_xor(sa, o, 64);
+        if (t == 0) bins[2 * kRadix] = sa;
+    }
     uint32_t tot;
     const uint32_t ex = block_excl_scan_tot<4>(v, s_w, &tot);  // (its barriers also publish s_c)
     bins[t] = ex + v;
@@ -403,8 +420,8 @@ int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s) {
         }
         sc.hist_cap = cap;
     }
-    if (!sc.row_total) {  // row totals [256] + tile counts [16][256] (zero between sorts)
-        const size_t bytes = (size_t)(1 + kTileCopies) * kRadix * 4;
+    if (!sc.row_total) {  // row totals [256] + tile counts [16][256] + above-1e6 counts [16] (zero between sorts)
+        const size_t bytes = ((size_t)(1 + kTileCopies) * kRadix + kTileCopies) * 4;
         if (hipMalloc(&sc.row_total, bytes) != hipSuccess || hipMemsetAsync(sc.row_total, 0, bytes, s) != hipSuccess) {
             err = "radix sort: out of device memory";
             return GS_ERR_NOMEM;

@@ -125,6 +125,24 @@ def expf(x: float) -> float:
     return lib().ora_expf(x)
 
 
+KEY_CULLED = np.float32(1000000.0).view(np.uint32)  # preprocess.glsl:83 depth of a culled splat
+
+
+def reference_draw_list(keys, vals, culled: int, flags: int):
+    """The sorted list the reference's draw walks (ref mode).  preprocess.glsl:80-88 leaves every
+    culled splat i in the sorted range with depth 1e6 and splatKeys[i] = 0, so after the sort it
+    sits, as splat 0 (draw.glsl:97-98 reads splatKeys[indices[pos]]), among the entries: after
+    every key whose bits are <= bits(1e6) (the emitted entries come first in the sort's input, so
+    equal keys keep them ahead), before the larger bit patterns (negative keys, Q6).  countBins
+    never bins 1e6, so only a Q10 over-read window reaches them.  `culled` = splats without
+    entries (NDC-culled; det == 0, Q7, is placed the same way).  Clean mode: no such entries."""
+    if flags & FLAG_CLEAN or culled <= 0:
+        return vals, len(vals)
+    P = int(np.searchsorted(keys, KEY_CULLED, side="right"))
+    out = np.concatenate([vals[:P], np.zeros(culled, np.uint32), vals[P:]])
+    return out, len(out)
+
+
 def render(means4, cov6, opacity, colours4, u, flags: int = 0, stages: bool = True, draw: bool = True):
     """Full frame in the oracle: preprocess -> emit -> stable sort -> bins -> draw.
     ``u`` is a gs_uniforms-like object (view, vp, width, height, focal_x, ...)."""
@@ -155,9 +173,10 @@ def render(means4, cov6, opacity, colours4, u, flags: int = 0, stages: bool = Tr
     bins = np.zeros(256, np.uint32)
     L.ora_bins(_p(keys), E, _p(bins))
     img = None
+    dvals, dE = reference_draw_list(keys, vals, n - int(cnt[0::2].sum()), flags)
     if draw:
         img = np.zeros((H, W, 4), np.uint8)
-        L.ora_draw(W, H, flags, _p(bins), _p(vals), E, _p(m2d), _p(conic), _p(colours4), _p(img))
+        L.ora_draw(W, H, flags, _p(bins), _p(dvals), dE, _p(m2d), _p(conic), _p(colours4), _p(img))
     out = dict(image=img, keys=keys, vals=vals, bins=bins, means2d=m2d, conics=conic, V=int(cnt[0::2].sum()),
                D=int(cnt[1::2].sum()), E=E, counts=cnt, z01=z01, tilexy=txy, rect=rect)
     if stages:
@@ -198,7 +217,8 @@ def time_frame(means4, cov6, opacity, colours4, u, flags: int = 0, row_step: int
     L.ora_bins(_p(keys), E, _p(bins))
     t3 = time.perf_counter()
     img = np.zeros((H, W, 4), np.uint8)
-    L.ora_draw_rows(W, H, flags, _p(bins), _p(vals), E, _p(m2d), _p(conic), _p(colours4), _p(img), 0, row_step)
+    dvals, dE = reference_draw_list(keys[:E], vals[:E], n - int(cnt[0::2].sum()), flags)
+    L.ora_draw_rows(W, H, flags, _p(bins), _p(dvals), dE, _p(m2d), _p(conic), _p(colours4), _p(img), 0, row_step)
     t4 = time.perf_counter()
     draw_full = (t4 - t3) * row_step
     total = (t1 - t0) + (t2 - t1) + (t3 - t2) + draw_full

@@ -58,9 +58,16 @@ def preprocess(means4, cov6, opacity, u, clean=False):
     return dict(culled=culled, sx=sx, sy=sy, z01=z01, conic=conic, det=det, radius=radius)
 
 
-def draw(W, H, vals_sorted, bins, means2d, conic4, colours4, clean=False, E=None):
-    """per-pixel front-to-back blend in float64 (no quirks beyond Q9/Q10 of ref mode)"""
-    E = len(vals_sorted) if E is None else E
+def draw(W, H, vals_sorted, bins, means2d, conic4, colours4, clean=False, E=None, keys_sorted=None, culled=0):
+    """per-pixel front-to-back blend in float64 (no quirks beyond Q9/Q10 of ref mode, and the
+    culled splats' 1e6 entries that a Q10 window can reach: given keys_sorted and the number of
+    culled splats, they are placed -- as splat 0 -- after the non-negative keys <= 1e6)"""
+    vals_sorted = np.asarray(vals_sorted)[: (len(vals_sorted) if E is None else E)]
+    if not clean and culled and keys_sorted is not None:
+        kf = np.asarray(keys_sorted[: len(vals_sorted)], np.uint32).view(np.float32)
+        P = int(np.count_nonzero(~np.signbit(kf) & (kf <= 1e6)))
+        vals_sorted = np.concatenate([vals_sorted[:P], np.zeros(culled, vals_sorted.dtype), vals_sorted[P:]])
+    E = len(vals_sorted)
     tw, th = W / 16.0, H / 16.0
     cw = W if clean else (W // 32) * 32
     ch = H if clean else (H // 32) * 32

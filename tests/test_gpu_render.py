@@ -195,3 +195,33 @@ def test_full_size_other_configs(ctx, oracle, W, H, view):
     for k in ("keys", "vals", "bins"):
         assert_bits(r[k], o[k], f"{W}x{H} view {view}/{k}")
     assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{W}x{H} view {view}/image")
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_culled_entries_drawn_as_splat_zero(oracle, staged):
+    """ref mode: the reference's culled splats stay in the sorted range as splat 0 (key 1e6,
+    preprocess.glsl:80-88) and a Q10 window reaches them (tests/culled_scene.py): bit-exact vs the
+    oracle, through the frame path (bins from the sort) and the staged one (k_bins_*)"""
+    from tests.culled_scene import culled_scene
+    W, H = 512, 512
+    ctx = g.Context(0)
+    means, col, op, log_sc, rot, u = culled_scene(g, W, H)
+    sp = g.Splats.from_raw(means, col, op, log_sc, rot, W, H, ctx=ctx)
+    ref = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0)
+    assert sp.numSplats - ref["V"] == 300
+    if staged:
+        sp._preprocess_u(u)
+        sp.sort()
+        sp.computeBins()
+        sp.draw(W, H, W / 16.0, H / 16.0)
+    else:
+        sp.render_uniforms(u)
+    assert np.array_equal(sp.texture(), ref["image"])
+    # splat 0 culled: its culled record never blends (the block changes nothing)
+    means2 = means.copy()
+    means2[0] = means[-1]
+    sp2 = g.Splats.from_raw(means2, col, op, log_sc, rot, W, H, ctx=ctx)
+    ref2 = oracle.render(sp2.means3D, sp2.covarianceMatrices, sp2.opacities, sp2.colours, u, flags=0)
+    sp2.render_uniforms(u)
+    assert np.array_equal(sp2.texture(), ref2["image"])
+    ctx.close()

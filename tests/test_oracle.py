@@ -209,7 +209,8 @@ def test_draw_oracle_vs_f64():
     for W, H, flags in ((96, 64, 1), (64, 64, 0)):
         u = g.main_camera(W, H).uniforms()
         r = O.render(means4, cov, opa, cols, u, flags=flags)
-        ref = ref_f64.draw(W, H, r["vals"], r["bins"], r["means2d"], r["conics"], cols, clean=bool(flags), E=r["E"])
+        ref = ref_f64.draw(W, H, r["vals"], r["bins"], r["means2d"], r["conics"], cols, clean=bool(flags), E=r["E"],
+                           keys_sorted=r["keys"], culled=len(opa) - r["V"])
         d = np.abs(r["image"].astype(int) - ref.astype(int))
         assert d.max() <= 2 and np.mean(d <= 1) >= 0.995, (W, H, d.max())
 
@@ -243,3 +244,32 @@ def test_golden_fixtures_reproduce(oracle, golden_dir, name):
         assert np.array_equal([r["V"], r["D"], r["E"]], z[f"{mode}_VDE"])
         for k in ("keys", "vals", "bins", "means2d", "conics", "image"):
             assert np.array_equal(r[k], z[f"{mode}_{k}"]), (mode, k)
+
+
+def test_culled_entries_reach_the_draw():
+    """preprocess.glsl:80-88 keeps culled splats in the sorted range (key 1e6, splatKeys = 0):
+    the last tile's Q10 window reads them as splat 0 in ref mode, which changes pixels; the
+    list is the emitted one with the block inserted after the keys <= 1e6"""
+    from oracle import oracle as O
+    import openglgaussiansplattingrenderer_amd as g
+    from tests.culled_scene import culled_scene
+    means, col, op, log_sc, rot, u = culled_scene(g)
+    cols, opa, scl, rt = g.activate(col, op, log_sc, rot)
+    means4 = np.concatenate([means, np.ones((len(means), 1), np.float32)], 1)
+    cov = O.cov3d(scl, rt)
+    r = O.render(means4, cov, opa, cols, u, flags=0)
+    culled = len(opa) - r["V"]
+    assert culled == 300
+    dvals, dE = O.reference_draw_list(r["keys"], r["vals"], culled, 0)
+    assert dE == r["E"] + culled and not dvals[r["E"]:].any()
+    # without the culled block the last tile's pixels differ
+    img_no = np.zeros_like(r["image"])
+    L = O.lib()
+    L.ora_draw(u.width, u.height, 0, O._p(r["bins"]), O._p(r["vals"]), r["E"], O._p(r["means2d"]),
+               O._p(r["conics"]), O._p(cols), O._p(img_no))
+    diff = np.any(img_no != r["image"], axis=2)
+    assert diff.sum() > 50, diff.sum()
+    assert not diff[: u.height // 2].any()  # the low tiles' windows end inside the list
+    # clean mode has no such entries
+    rc = O.render(means4, cov, opa, cols, u, flags=1)
+    assert O.reference_draw_list(rc["keys"], rc["vals"], culled, 1)[1] == rc["E"]
