@@ -37,14 +37,24 @@ inline int report(int rc, const gs_ctx *ctx = nullptr) {
     return rc;
 }
 
-// One GPU: replaces the GL context + compiled programs.
+// One GPU: replaces the GL context + compiled programs.  Like a GL context it can be made
+// current on the calling thread (the first one created is), so the reference's context-free
+// calls -- GPURadixSort's 10-argument form -- find it.
 class Context {
   public:
-    explicit Context(int device = 0) { report(gs_ctx_create(device, &ctx_)); }
-    ~Context() { gs_ctx_destroy(ctx_); }
+    explicit Context(int device = 0) {
+        report(gs_ctx_create(device, &ctx_));
+        if (!current_slot()) current_slot() = this;
+    }
+    ~Context() {
+        if (current_slot() == this) current_slot() = nullptr;
+        gs_ctx_destroy(ctx_);
+    }
     Context(const Context &) = delete;
     Context &operator=(const Context &) = delete;
     gs_ctx *get() const { return ctx_; }
+    void makeCurrent() { current_slot() = this; }          // glfwMakeContextCurrent
+    static Context *current() { return current_slot(); }    // or null
     void finish() const { report(gs_sync(ctx_), ctx_); }  // glFinish
     // frames in flight on the device: 2 (default; frame k+1's preprocess / emission / sort
     // overlap frame k's blend), 3 (one more in flight), or 1 (one frame at a time, as
@@ -52,6 +62,10 @@ class Context {
     int setLanes(int lanes) const { return report(gs_ctx_set_lanes(ctx_, lanes), ctx_); }
 
   private:
+    static Context *&current_slot() {
+        static thread_local Context *cur = nullptr;
+        return cur;
+    }
     gs_ctx *ctx_ = nullptr;
 };
 
@@ -82,6 +96,21 @@ inline int GPURadixSort(const Context &ctx, unsigned /*histogramProgram*/, unsig
         return GS_ERR_INVALID;
     }
     return report(gs_argsort_f32(ctx.get(), keysBuffer, orderBuffer, size), ctx.get());
+}
+
+// include/sort.h:18-20, the reference's exact arity: the sort runs on the thread's current
+// Context (as the GL calls run on the current GL context), so tests/sortTests.cpp:215 compiles
+// with device pointers in place of the GL buffer handles.
+inline int GPURadixSort(unsigned histogramProgram, unsigned prefixSumProgram, unsigned sortProgram,
+                        void *intermediateBuffer, int32_t *orderBuffer, void *histogramBuffer, int size,
+                        int workGroupCount, int workGroupSize, const float *buffer) {
+    Context *ctx = Context::current();
+    if (!ctx) {
+        std::cerr << "Error: GPURadixSort: no current context" << std::endl;
+        return GS_ERR_STATE;
+    }
+    return GPURadixSort(*ctx, histogramProgram, prefixSumProgram, sortProgram, intermediateBuffer, orderBuffer,
+                        histogramBuffer, size, workGroupCount, workGroupSize, buffer);
 }
 
 // include/Splats.h:29-124

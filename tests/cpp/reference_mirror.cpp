@@ -48,7 +48,8 @@ static int sort_test(gs::Context &ctx) {
     EXPECT(gs_memcpy_h2d(ctx.get(), keys, randomNumbers.data(), size * 4) == GS_OK);
     EXPECT(gs_memcpy_h2d(ctx.get(), order, ascending.data(), size * 4) == GS_OK);
     auto t0 = std::chrono::steady_clock::now();
-    EXPECT(gs::GPURadixSort(ctx, hp, up, sp, nullptr, (int32_t *)order, nullptr, size, 16, 32, (const float *)keys) ==
+    // sortTests.cpp:215, the reference's 10 arguments (the thread's current context)
+    EXPECT(gs::GPURadixSort(hp, up, sp, nullptr, (int32_t *)order, nullptr, size, 16, 32, (const float *)keys) ==
            GS_OK);
     ctx.finish();
     auto t1 = std::chrono::steady_clock::now();

@@ -3,8 +3,10 @@ separate passes, as MI355X_MICROARCH.md prescribes).
 
 FETCH_SIZE/WRITE_SIZE are in KiB per dispatch.  gfx950 correction: FETCH_SIZE counts 128-B
 streaming requests at 64 B (reads 1/2 of a wide coalesced stream), so for kernels whose reads
-are wide coalesced streams the fetch is doubled; the blend's reads are 4-16-B random gathers
-(64-B requests, counted exactly), so its fetch is used as-is.  Both numbers are recorded.
+are wide coalesced streams the fetch is doubled.  The blend's reads are 4-32-B random gathers:
+calibrated on a known byte count (tools/micro/gather.hip + gather_pmc.sh ->
+profiles/r02/calibration.txt), each such gather that misses L2 is tallied as exactly one 64-B
+request, so its fetch is used as-is (x1).  Both numbers are recorded.
 usage: python tools/pmc_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv out.json
 """
 import collections
