@@ -41,20 +41,29 @@ __device__ __forceinline__ int f2i(float f) {
     return r;
 }
 
-// mask of the active lanes whose 8-bit digit equals this lane's (8 ballots).  Per bit:
-// s = the lane's bit sign-extended, m &= ~(ballot ^ s) -- one v_bitop3 per mask half
-// (4 VALU per bit instead of the 6-8 a per-lane select costs).
+// mask of the active lanes whose 8-bit digit equals this lane's (8 ballots).  Per bit: s = the
+// lane's bit sign-extended (v_bfe_i32), the ballot of it, and the lanes that differ accumulate
+// as x |= ballot ^ s -- one v_bitop3 per mask half and bit, written out (left to itself the
+// compiler pairs the xors into v_or3, three VALU per two bits and half instead of two);
+// the match is ~x & active.  4 VALU per bit.
+__device__ __forceinline__ uint32_t or_xor(uint32_t acc, uint32_t s, uint32_t ballot_half) {
+    // acc | (s ^ ballot_half): the table is the expression evaluated on src0 = 0xf0, src1 = 0xcc,
+    // src2 = 0xaa: 0xf0 | (0xcc ^ 0xaa) = 0xf6 (checked on the GPU: tools/micro/bitop3_check.hip).
+    // The builtin, not inline asm: the compiler then also inserts the wait states a VALU read of
+    // the just-written ballot SGPR needs (the inline-asm form missed them and mis-sorted)
+    return __builtin_amdgcn_bitop3_b32(acc, s, ballot_half, 0xf6);
+}
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
-    uint32_t lo = (uint32_t)active, hi = (uint32_t)(active >> 32);
+    uint32_t xlo = 0, xhi = 0;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         uint32_t sb = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);  // v_bfe_i32
         asm volatile("" : "+v"(sb));  // keep the compare on sb (no shift + compare rewrite)
         const uint64_t bb = __ballot(sb != 0u);
-        lo &= ~((uint32_t)bb ^ sb);
-        hi &= ~((uint32_t)(bb >> 32) ^ sb);
+        xlo = or_xor(xlo, sb, (uint32_t)bb);
+        xhi = or_xor(xhi, sb, (uint32_t)(bb >> 32));
     }
-    return ((uint64_t)hi << 32) | lo;
+    return (((uint64_t)~xhi << 32) | ~xlo) & active;
 }
 
 // number of set bits of m below this lane (v_mbcnt)
