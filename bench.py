@@ -182,17 +182,37 @@ def cpu_baseline(sp, u, flags, budget_s: float = 20.0):
                 detail=r)
 
 
-def load_pmc(kernel: str):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary (FETCH_SIZE doubled per
-    the gfx950 correction + WRITE_SIZE), or None."""
+def load_pmc(kernel: str, field: str = "hbm_bytes_per_launch"):
+    """From the committed rocprofv3 PMC summary (profiles/pmc_summary.json, tools/collect_profiles.sh):
+    HBM traffic per launch (FETCH_SIZE x2 for streams, x1 for the blend's calibrated gathers,
+    + WRITE_SIZE), or another field ("sq": the SQ counters per dispatch); None if absent."""
     p = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(p):
         return None
     try:
         d = json.load(open(p))
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get(kernel, {}).get(field)
     except Exception:
         return None
+
+
+SIMDS = 1024            # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+CLOCK_GHZ = 2.4         # peak engine clock
+VALU_CYC = 2            # cycles per wave64 VALU instruction at full issue (v_fma_f32 row)
+
+
+def issue_ceiling(kernel: str, launch_ms: float):
+    """The blend is bound by instruction issue, not HBM: its VALU instructions per launch (SQ
+    pass) at one wave64 VALU per SIMD every 2 cycles on all 1024 SIMDs at 2.4 GHz give the
+    issue ceiling; frac = ceiling / measured launch time."""
+    sq = load_pmc(kernel, "sq")
+    if not sq or not sq.get("SQ_INSTS_VALU"):
+        return None
+    v = float(sq["SQ_INSTS_VALU"])
+    ceil_ms = v * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e9) * 1e3
+    return {"valu_insts_per_launch": v, "salu_insts_per_launch": sq.get("SQ_INSTS_SALU"),
+            "ceiling_ms": round(ceil_ms, 4), "frac": round(ceil_ms / launch_ms, 4),
+            "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cyc / (1024 SIMDs x 2.4 GHz)"}
 
 
 def main():
@@ -329,7 +349,9 @@ def main():
         "draw": 40 * E + 4 * W * H,
     }
     draw_ms_live = tm_draw["ms_draw"] / max(1, tm_draw["frames"])  # timed region, HIP events
-    dom = max(stage_ms, key=lambda k: stage_ms[k])
+    # the dominant kernel: the blend (the longest stage alone; with ranks sharing one GPU the
+    # stage-timing pass overlaps other ranks' work, so this is not re-derived per run)
+    dom = "draw"
     if dom == "draw":
         stage_ms_dom = draw_ms_live
     else:
@@ -350,6 +372,7 @@ def main():
         roofline["one_frame"] = {"avg_launch_ms": round(one_ms, 4), "achieved": round(one, 2),
                                  "frac": round(one / HBM_PEAK_GBS, 4),
                                  "source": "hipEvents on the draw dispatch, frames one at a time (1 lane)"}
+        roofline["issue"] = issue_ceiling(kern_name, one_ms)
     frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
     frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
 
