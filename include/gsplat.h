@@ -98,6 +98,19 @@ void *gs_stream(gs_ctx *ctx);                /* the hipStream_t of the newest fr
  * may overlap; everything else behaves as one stream) -- or 1.
  * Beyond the reference, whose gpuRender blocks per frame (src/Splats.cpp:580,595). */
 int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
+/* Prefix sort of frames enqueued without a host round trip (beyond the reference, whose
+ * GPURadixSort orders every entry, src/sort.cpp:139-203): each tile's list is sorted at least
+ * `target` entries deep (default 32768; the blend reads ~2-20k of lists up to 0.8M long at
+ * C3) and the rest of it is left unsorted.  Images are unchanged: a frame whose blend reaches
+ * an unsorted position before saturating is rendered again with the full sort, and the target
+ * doubles for the frames after it.  target 0: always the full sort.  Frames with fewer than
+ * 64 * target entries (the previous frame's count) use the full sort.  Returns the current
+ * target in *current when it is not NULL (with target < 0: only that). */
+int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current);
+/* prefix-sort counters: [0] frames prefix-sorted, [1] of them rendered again (a blend reached
+ * an unsorted position), [2] entries kept by the newest retired prefix-sorted frame, [3] its
+ * entry count; reset != 0 clears [0] and [1] */
+int gs_prefix_stats(gs_ctx *ctx, uint64_t out[4], int reset);
 
 /* device memory helpers (callers without their own allocator, e.g. ctypes tests) */
 int gs_malloc(gs_ctx *ctx, size_t bytes, void **dptr);

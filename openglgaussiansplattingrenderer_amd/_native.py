@@ -112,6 +112,8 @@ SIGNATURES = {
     "gs_sync": (_i, [_vp]),
     "gs_stream": (_vp, [_vp]),
     "gs_ctx_set_lanes": (_i, [_vp, _i]),
+    "gs_ctx_set_sort_prefix": (_i, [_vp, _i, ctypes.POINTER(_i)]),
+    "gs_prefix_stats": (_i, [_vp, _vp, _i]),
     "gs_malloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
     "gs_free": (_i, [_vp, _vp]),
     "gs_memcpy_h2d": (_i, [_vp, _vp, _vp, _sz]),

@@ -43,6 +43,8 @@ struct Lane {
     uint32_t *keys = nullptr, *vals = nullptr;
     uint32_t *vals_base = nullptr;  // the allocation: kValsPad zero words, then vals (k_draw reads vals[-1] = 0)
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
+    bool vals_partial = false;  // the frame was prefix-sorted: vals holds only each list's sorted prefix
+    uint32_t *pre_buf = nullptr;  // prefix-sort state (gs::kPrefixWords words, see gs::PrefixDev)
     gs::SortScratch sort;
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
@@ -92,6 +94,7 @@ struct gs_ctx {
         int lane = -1;
         const void *draw_out = nullptr;
         bool drawn = false, draw_stats = false;
+        bool prefix = false;  // prefix-sorted: its blend may flag a miss (ring word 2)
     };
     Slot slot[kRing];
     hipEvent_t ev[kRing][kEv] = {};
@@ -107,6 +110,9 @@ struct gs_ctx {
     bool e_known = false;        // an entry count has been observed (sizes speculative frames)
     gs_timing acc = {};
     bool in_render = false;      // inside gs_render: host waits count as ms_host_wait
+    // prefix sort (gs_ctx_set_sort_prefix)
+    int prefix_target = 32768;
+    uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
 };
 
 struct gs_scene {
@@ -277,6 +283,7 @@ hipEvent_t fev(gs_ctx *ctx, int i) {
 
 int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out,
                 int out_on_device, gs_frame_stats *stats);
+int resort_full(gs_ctx *ctx);
 
 int oldest_used(const gs_ctx *ctx, uint64_t seq_limit) {
     int k = -1;
@@ -322,7 +329,18 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
         }
         if (sl.spec) {
             const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
-            if (V + D > sl.cap) return handle_overflow(ctx);
+            // a prefix-sorted frame whose blend reached an unsorted position: render it again
+            // (full sort) and sort deeper from now on
+            const bool miss = sl.prefix && ctx->h_ring[4 * k + 2] != 0;
+            if (miss) {
+                ctx->prefix_redo += 1;
+                ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
+            }
+            if (V + D > sl.cap || miss) return handle_overflow(ctx);
+            if (sl.prefix) {
+                ctx->prefix_kept = ctx->h_ring[4 * k + 3];
+                ctx->prefix_E = (uint64_t)(V + D);
+            }
             ctx->V = V;
             ctx->D = D;
             ctx->E = V + D;
@@ -446,7 +464,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
         void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
-                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col};
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
@@ -824,6 +842,7 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
 
 int enqueue_emit(gs_ctx *ctx) {
     ctx->L->keys_sorted = true;  // emission order, as gs_frame_read shows it before gs_sort
+    ctx->L->vals_partial = false;
     gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
                     fev(ctx, 3));
     GS_HIP(ctx, hipGetLastError());
@@ -835,12 +854,14 @@ int enqueue_emit(gs_ctx *ctx) {
 // the bins stage is then empty (its timing event follows the sort's)
 // A frame sort with bins leaves the keys unsorted (the blend reads the values and the bins
 // only) when the splat ids fit 24 bits; gs_frame_read(GS_READ_KEYS) then sorts again.
-int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false) {
-    const bool keys_out = !with_bins || ctx->n > (1 << 24);
+int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false,
+                 const gs::PrefixDev *pre = nullptr) {
+    const bool keys_out = !pre && (!with_bins || ctx->n > (1 << 24));
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out))
+                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre))
         return set_error(ctx, rc, ctx->err);
     ctx->L->keys_sorted = keys_out;
+    ctx->L->vals_partial = pre != nullptr;
     if (with_bins)
         if (hipEvent_t e = fev(ctx, 6)) GS_HIP(ctx, hipEventRecord(e, ctx->L->stream));
     return GS_OK;
@@ -853,7 +874,8 @@ int enqueue_bins(gs_ctx *ctx, int64_t E, const uint32_t *count) {
 }
 
 int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float tile_w, float tile_h,
-                 uint32_t flags, void *out_rgba8, int out_on_device, int64_t E, const uint32_t *count) {
+                 uint32_t flags, void *out_rgba8, int out_on_device, int64_t E, const uint32_t *count,
+                 bool prefix = false) {
     const bool clean = (flags & GS_FLAG_CLEAN) != 0;
     gs::DrawParams P;
     P.W = width;
@@ -899,6 +921,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.coverH = coverH;
     P.n = scene->n;
     P.V = (int32_t)ctx->V;  // used when count is null (the frame's counts are on the host)
+    P.prefix = prefix ? 1 : 0;
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other
@@ -957,11 +980,33 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     sl.out = out;
     sl.cap = ctx->L->e_cap;
     const uint32_t *cnt = ctx->L->totals;
+    // prefix sort: frames of the size where the lists are long (the last observed count)
+    const bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_target;
+    gs::PrefixDev pd{};
+    if (prefix) {
+        if (!ctx->L->pre_buf) {
+            GS_HIP(ctx, hipMalloc(&ctx->L->pre_buf, gs::kPrefixWords * 4));
+            GS_HIP(ctx, hipMemsetAsync(ctx->L->pre_buf, 0, gs::kPrefixWords * 4, ctx->L->stream));
+        }
+        uint32_t *b = ctx->L->pre_buf;
+        pd.hist = b;
+        pd.theta = pd.hist + (size_t)gs::kPrefixHistCopies * 256 * gs::kPrefixBuckets;
+        pd.counts = pd.theta + gs::kClasses;
+        pd.nsel = pd.counts + (size_t)gs::kPrefixCopies * (gs::kClasses + 1);
+        pd.delta = (int32_t *)(pd.nsel + 2);
+        pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
+        pd.target = (uint32_t)ctx->prefix_target;
+        pd.n = scene->n;
+        pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
+        sl.prefix = true;
+        ctx->prefix_frames += 1;
+    }
     int rc;
-    if ((rc = enqueue_emit(ctx)) || (rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true)))
+    if ((rc = enqueue_emit(ctx)) ||
+        (rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr)))
         return rc;
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
-                           out, 1, ctx->L->e_cap, cnt)))
+                           out, 1, ctx->L->e_cap, cnt, prefix)))
         return rc;
     ctx->stage = 3;
     return GS_OK;
@@ -1002,6 +1047,7 @@ int gs_sort(gs_ctx *ctx) {
     if (int rc = validate_all(ctx)) return rc;
     if (ctx->stage < 1) return set_error(ctx, GS_ERR_STATE, "gs_sort: call gs_preprocess first");
     if (int rc = use_device(ctx)) return rc;
+    if (int rc = resort_full(ctx)) return rc;  // consistent (key, value) pairs after a frame sort
     if (int rc = enqueue_sort(ctx, ctx->E, nullptr)) return rc;
     ctx->stage = 2;
     return GS_OK;
@@ -1012,6 +1058,8 @@ int gs_compute_bins(gs_ctx *ctx) {
     if (int rc = validate_all(ctx)) return rc;
     if (ctx->stage < 2) return set_error(ctx, GS_ERR_STATE, "gs_compute_bins: call gs_sort first");
     if (int rc = use_device(ctx)) return rc;
+    if (ctx->L->vals_partial)
+        if (int rc = resort_full(ctx)) return rc;  // (a prefix sort left the keys buffer as scratch)
     if (int rc = enqueue_bins(ctx, ctx->E, nullptr)) return rc;
     ctx->stage = 3;
     return GS_OK;
@@ -1025,6 +1073,8 @@ int gs_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, float til
     if (width <= 0 || height <= 0) return set_error(ctx, GS_ERR_INVALID, "gs_draw: bad resolution");
     if (scene->n != ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_draw: scene differs from the preprocessed one");
     if (int rc = use_device(ctx)) return rc;
+    if (ctx->L->vals_partial)  // the whole sorted lists for a draw of them (the bins are exact)
+        if (int rc = resort_full(ctx)) return rc;
     return enqueue_draw(ctx, scene, width, height, tile_w, tile_h, flags, out_rgba8, out_on_device, ctx->E, nullptr);
 }
 
@@ -1085,6 +1135,45 @@ int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats) {
     return GS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// The newest frame's entries again, emitted and sorted with their keys: after a frame sort
+// that left the keys unsorted (keys_sorted false) or sorted only each list's prefix
+// (vals_partial), for the stage calls and readbacks that need the whole sorted pairs.
+int resort_full(gs_ctx *ctx) {
+    if (ctx->stage < 2 || (ctx->L->keys_sorted && !ctx->L->vals_partial)) return GS_OK;
+    gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals,
+                    (uint32_t)ctx->L->e_cap, nullptr, nullptr);
+    GS_HIP(ctx, hipGetLastError());
+    if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, ctx->E, ctx->err))
+        return set_error(ctx, rc, ctx->err);
+    ctx->L->keys_sorted = true;
+    ctx->L->vals_partial = false;
+    return GS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (target >= 0) ctx->prefix_target = target;
+    if (current) *current = ctx->prefix_target;
+    return GS_OK;
+}
+
+int gs_prefix_stats(gs_ctx *ctx, uint64_t out[4], int reset) {
+    if (!ctx || !out) return set_error(ctx, GS_ERR_INVALID, "gs_prefix_stats: null argument");
+    if (int rc = gs_sync(ctx)) return rc;
+    out[0] = ctx->prefix_frames;
+    out[1] = ctx->prefix_redo;
+    out[2] = ctx->prefix_kept;
+    out[3] = ctx->prefix_E;
+    if (reset) ctx->prefix_frames = ctx->prefix_redo = 0;
+    return GS_OK;
+}
+
 int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     if (!ctx || (!host_dst && count)) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: null argument");
     if (int rc = gs_sync(ctx)) return rc;
@@ -1108,16 +1197,12 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
     };
     switch (what) {
     case GS_READ_KEYS:
-        if (!ctx->L->keys_sorted && ctx->stage >= 2) {  // the frame's entries again, sorted with their keys
-            gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals,
-                            (uint32_t)ctx->L->e_cap, nullptr, nullptr);
-            GS_HIP(ctx, hipGetLastError());
-            if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, ctx->E, ctx->err))
-                return set_error(ctx, rc, ctx->err);
-            ctx->L->keys_sorted = true;
-        }
+        if (int rc = resort_full(ctx)) return rc;  // the frame's entries again, sorted with their keys
         src = ctx->L->keys; avail = (size_t)ctx->E; break;
-    case GS_READ_VALS: src = ctx->L->vals; avail = (size_t)ctx->E; break;
+    case GS_READ_VALS:
+        if (ctx->L->vals_partial)
+            if (int rc = resort_full(ctx)) return rc;
+        src = ctx->L->vals; avail = (size_t)ctx->E; break;
     case GS_READ_BINS:
         if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");
         src = ctx->L->bins; avail = 256; break;

@@ -40,8 +40,72 @@ constexpr int kTiles = 16;  // the reference's fixed 16x16 coarse grid (preproce
 // (k_draw places them virtually; bins[512] = the number of entries with larger key bits)
 constexpr uint32_t kKeyCulledBits = 0x49742400u;
 constexpr int kValsPad = 16;         // zero words before a frame's sorted values (vals[-1] = splat 0)
-constexpr int kBinsWords = 520;      // bins buffer: [256] tile ends, [256] draw order, [512] keys above 1e6
+// bins buffer: [256] tile ends, [256] draw order, [512] keys above 1e6, then (prefix-sorted
+// frames) [kBinsLimit + t] the first list position of tile t's window that is not sorted
+constexpr int kBinsLimit = 520;
+constexpr int kBinsWords = kBinsLimit + 256;
 constexpr int kBinCountWords = 260;  // counts of k_bins_count: [0, 256) tiles, [256] keys above 1e6
+
+// ------------------------------------------------------------ prefix sort of a frame
+// A frame's blend reads each tile's sorted list only up to where its sub-blocks saturate: at
+// C3 (1080p, 6.1M splats) 8 % of the 10M entries (the longest lists, 0.3-0.8M entries, are
+// read for their first 2-3k).  A frame enqueued without a host round trip therefore sorts a
+// prefix of every list (gs_sort.hip, "prefix sort"):
+//   * key classes: c = t for keys in [t, t+1) (t = 0..255, the tile lists of the bins), and
+//     c = 256 for every other bit pattern (>= 256, inf, NaN, negative), always kept whole;
+//   * k_prefix_sample adds one emitted key in kPrefixSample to a per-class histogram of the
+//     distance d = bits(t + 1) - key (floating-point buckets: 5-bit exponent, 6-bit mantissa;
+//     kPrefixHistCopies copies, so the few hot buckets of a deep list do not serialise);
+//   * k_prefix_select picks per class the largest key bound whose sampled count reaches
+//     target / kPrefixSample (or keeps the class whole);
+//   * the first sort pass keeps the keys at or below their class bound (stable), the other
+//     passes sort that subset, and the last one writes each value at its position in the full
+//     sorted order (class start in the full order - class start in the subset);
+//   * the bins workgroup stores per tile the first position of its draw window that was not
+//     sorted (bins[kBinsLimit + t]); a sub-block that reaches it unsaturated flags the frame
+//     (pinned ring word 2), which is then rendered again with the full sort.
+constexpr int kClasses = 257;
+constexpr int kPrefixBuckets = 2048;
+constexpr int kPrefixSample = 64;
+constexpr int kPrefixHistCopies = 8;
+constexpr int kPrefixCopies = 16;  // selected-count copies (spread same-address atomics)
+struct PrefixDev {
+    uint32_t *hist;    // [kPrefixHistCopies][256][kPrefixBuckets] sampled counts (zero between frames)
+    uint32_t *theta;   // [kClasses] inclusive key bound of the kept keys
+    uint32_t *counts;  // [kPrefixCopies][kClasses] kept per class, then [kPrefixCopies] keys < 1.0 (zero between frames)
+    uint32_t *nsel;    // [2]: kept keys, 0 (the element count of passes 1-3)
+    int32_t *delta;    // [kClasses]: full-order start - subset start of each class
+    uint32_t *h_slot;  // mapped pinned ring slot of the frame: [3] = kept keys (diagnostics), or null
+    uint32_t target;   // entries per class to keep at least
+    int32_t n;         // splats of the scene (the reference's culled entries: n - V)
+    int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
+};
+constexpr uint32_t kKey1Bits = 0x3f800000u;    // bits(1.0f)
+constexpr uint32_t kKey256Bits = 0x43800000u;  // bits(256.0f)
+// key class: t for the keys in [t, t+1), t < 256; 256 for every other bit pattern
+__device__ __forceinline__ uint32_t key_class(uint32_t k) {
+    return k < kKey256Bits ? (uint32_t)__uint_as_float(k) : 256u;  // (a float in [0, 256): truncation)
+}
+// bits of the upper bound t + 1 of tile class t
+__host__ __device__ inline uint32_t class_hi(uint32_t t) {
+    const float f = (float)(t + 1);
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    return u;
+}
+// histogram bucket of a distance d >= 1 below the class bound: monotone, 6 mantissa bits
+// (d < 2^30: buckets < 30 * 64 = 1920)
+__device__ __forceinline__ uint32_t prefix_bucket(uint32_t d) {
+    const uint32_t e = 31u - (uint32_t)__builtin_clz(d);
+    const uint32_t m = e >= 6 ? (d >> (e - 6)) & 63u : (d << (6 - e)) & 63u;
+    return (e << 6) | m;
+}
+// the smallest d in bucket b
+__host__ __device__ inline uint32_t prefix_bucket_dmin(uint32_t b) {
+    const uint32_t e = b >> 6, m = 64u | (b & 63u);
+    return e >= 6 ? m << (e - 6) : m >> (6 - e);
+}
+constexpr size_t kPrefixWords = (size_t)kPrefixHistCopies * 256 * kPrefixBuckets + kClasses + (size_t)kPrefixCopies * (kClasses + 1) + 2 + kClasses;
 
 // Per-frame uniforms of the preprocess kernel (preprocess.glsl:18-37)
 struct PreParams {
@@ -67,6 +131,7 @@ struct DrawParams {
     int32_t coverW, coverH;     // drawn coverage; pixels outside it are zeroed (Q9)
     int32_t n;                  // splats of the scene
     int32_t V;                  // splats with entries (when count is null; else count[0])
+    int32_t prefix;             // prefix-sorted frame: windows end at bins[kBinsLimit + t] (a miss flags fr.h_totals[2])
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };
@@ -89,9 +154,11 @@ struct SortScratch {
 // keys_out false (values < 2^24 required): only the values come out sorted -- the last two
 // passes move one packed word (top key byte | value) instead of the pair; keys is left holding
 // an intermediate order.
+// pre != null (with bins and dev_count): the frame's prefix sort (see PrefixDev): vals holds
+// the sorted values at the positions bins[kBinsLimit + t] marks as sorted, keys are not output.
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
-               uint32_t *bins = nullptr, bool keys_out = true);
+               uint32_t *bins = nullptr, bool keys_out = true, const PrefixDev *pre = nullptr);
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]

@@ -389,6 +389,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, in
         if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
             fr.h_totals[0] = s_carry[0];
             fr.h_totals[1] = s_carry[1];
+            fr.h_totals[2] = 0;  // the prefix-sort miss flag (k_draw)
+            fr.h_totals[3] = 0;
         }
     }
 }
@@ -677,7 +679,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                                              const uint32_t *__restrict__ vals,
                                              const uint2 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
-                                             uint32_t *__restrict__ out, unsigned long long *__restrict__ stats) {
+                                             uint32_t *__restrict__ out, unsigned long long *__restrict__ stats,
+                                             uint32_t *fr_h_totals) {
     // pixel state, pixel id = 4*lane + slot; a pixel is done (:129-133) iff its w >= 0.99 (pixels
     // outside the image start at w = 1)
     __shared__ float4 s_col[256];
@@ -741,6 +744,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         const int chunks = (end - start + 1023) / 1024;
         end = min(E + cn, start + chunks * 1024);
     }
+    // prefix-sorted frame: positions from bins[kBinsLimit + t] on were not sorted; a block that
+    // gets there before saturating flags the frame (rendered again with the full sort)
+    const int wend = end;
+    if (P.prefix) end = min(end, (int)min(bins[kBinsLimit + t], 0x7fffffffu));
     const int qmax = max(E - 1, 0);
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
@@ -1067,6 +1074,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             if (!step(std::integral_constant<int, 1>{})) break;
         }
     }
+    if (P.prefix && end < wend && !all_done && fr_h_totals) fr_h_totals[2] = 1u;  // (uniform) a prefix miss
     if (sparse && (uint32_t)lane < nact) s_col[spix] = pc;  // the sparse phase's state (distinct pixels)
     wave_lds_sync();
     {  // the quad's pixels again from the lane id (v_mbcnt, which the compiler does not merge with
@@ -1144,7 +1152,7 @@ void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32
     const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
 #define GS_DRAW(F, S)                                                                                         \
     hipExtLaunchKernelGGL((k_draw<F, S>), grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, \
-                          colour, out, stats)
+                          colour, out, stats, fr.h_totals)
     if (stats) {
         if (fast_exp) GS_DRAW(true, true);
         else GS_DRAW(false, true);

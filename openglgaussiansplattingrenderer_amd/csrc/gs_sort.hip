@@ -135,11 +135,14 @@ __host__ __device__ constexpr uint32_t xcd_grid(uint32_t nb) { return 8 * ((nb +
 // digits leave short runs per tile, so a larger tile doubles the scatter's write runs)
 // tile_counts != null: also countBins.glsl:20-31 -- tile_counts[int(key)] += 1 for int(key) in
 // [0, 256), LDS replicas, then one global atomic per nonzero tile and workgroup
-template <int W, bool TILES>
+// PREFIX (the first pass of a frame's prefix sort): only the keys at or below their class
+// bound (PrefixDev::theta) are counted for the digits; the tile counts (TILES) stay over every
+// key; the kept keys per class and the keys below 1.0 (class 0's total) go to pre.counts
+template <int W, bool TILES, bool PREFIX = false>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
-                                                    uint32_t *__restrict__ tile_counts) {
+                                                    uint32_t *__restrict__ tile_counts, PrefixDev pre) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems;
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
@@ -150,9 +153,17 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     __shared__ uint32_t s_cnt[kRadix * kRep];
     __shared__ uint32_t s_tiles[TILES ? kRadix * kRep : 1];
     __shared__ uint32_t s_above;
+    __shared__ uint32_t s_theta[PREFIX ? kClasses : 1];
+    __shared__ uint32_t s_sel[PREFIX ? kClasses * kRep : 1];
+    __shared__ uint32_t s_low;
     for (int i = threadIdx.x; i < kRadix * kRep; i += kThreads) {
         s_cnt[i] = 0;
         if (TILES) s_tiles[i] = 0;
+    }
+    if (PREFIX) {
+        for (int i = threadIdx.x; i < kClasses * kRep; i += kThreads) s_sel[i] = 0;
+        for (int i = threadIdx.x; i < kClasses; i += kThreads) s_theta[i] = pre.theta[i];
+        if (threadIdx.x == 0) s_low = 0;
     }
     if (TILES && threadIdx.x == 0) s_above = 0;
     __syncthreads();
@@ -171,12 +182,19 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         }
     }
     const uint32_t rep = (uint32_t)lane & (kRep - 1);
-    uint32_t above = 0;
+    uint32_t above = 0, low = 0;
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
         if (idx < n) {
-            atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
+            bool keep = true;
+            if (PREFIX) {
+                const uint32_t c = key_class(kk[k]);
+                keep = kk[k] <= s_theta[c];
+                if (keep) atomicAdd(&s_sel[c * kRep + rep], 1u);
+                low += kk[k] < kKey1Bits ? 1u : 0u;
+            }
+            if (keep) atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
             if (TILES) {  // the frame's tile counts ride on the first pass
                 const uint32_t t = (uint32_t)f2i(__uint_as_float(kk[k]));
                 if (t < (uint32_t)kRadix) atomicAdd(&s_tiles[t * kRep + rep], 1u);
@@ -188,15 +206,27 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
         above = wave_incl_scan(above);
         if (lane == 63 && above) atomicAdd(&s_above, above);
     }
+    if (PREFIX) {
+        low = wave_incl_scan(low);
+        if (lane == 63 && low) atomicAdd(&s_low, low);
+    }
     __syncthreads();
     if (TILES && threadIdx.x == 0 && s_above) atomicAdd(&tile_counts[kTileCopies * kRadix + (blockIdx.x % kTileCopies)], s_above);
-    const int d = threadIdx.x;
-    if (d >= kRadix) return;
     auto sum8 = [](const uint32_t *p) {
         const uint4 c0 = *reinterpret_cast<const uint4 *>(p);
         const uint4 c1 = *reinterpret_cast<const uint4 *>(p + 4);
         return (c0.x + c0.y + c0.z + c0.w) + (c1.x + c1.y + c1.z + c1.w);
     };
+    if (PREFIX) {
+        uint32_t *pc = pre.counts + (blockIdx.x % kPrefixCopies) * kClasses;
+        for (int c = threadIdx.x; c < kClasses; c += kThreads) {
+            const uint32_t v = sum8(&s_sel[c * kRep]);
+            if (v) atomicAdd(&pc[c], v);
+        }
+        if (threadIdx.x == 0 && s_low) atomicAdd(&pre.counts[kPrefixCopies * kClasses + (blockIdx.x % kPrefixCopies)], s_low);
+    }
+    const int d = threadIdx.x;
+    if (d >= kRadix) return;
     hist[(size_t)d * nb + tile] = sum8(&s_cnt[d * kRep]);
     if (TILES) {
         const uint32_t c = sum8(&s_tiles[d * kRep]);
@@ -207,7 +237,9 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
 // tile bins from the tile counts (one workgroup of 256): bins[t] = inclusive prefix, and the
 // draw's tile order bins[256 + r] = the tile with the r-th longest list (ties by index); the
 // counts are cleared for the next frame
-__device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w) {
+// (returns the tile's count and the exclusive prefix; *s_above gets the keys above 1e6)
+__device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w,
+                           uint32_t *s_above) {
     __shared__ uint32_t s_c[kRadix];
     const int t = threadIdx.x;
     uint32_t v = 0;
@@ -223,7 +255,10 @@ __device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ 
         uint32_t sa = a;
 #pragma unroll
         for (int o = 1; o < kTileCopies; o <<= 1) sa += __shfl_xor(sa, o, 64);
-        if (t == 0) bins[2 * kRadix] = sa;
+        if (t == 0) {
+            bins[2 * kRadix] = sa;
+            *s_above = sa;
+        }
     }
     uint32_t tot;
     const uint32_t ex = block_excl_scan_tot<4>(v, s_w, &tot);  // (its barriers also publish s_c)
@@ -236,6 +271,94 @@ __device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ 
         r += (c > v || (c == v && u < t)) ? 1u : 0u;
     }
     bins[kRadix + r] = (uint32_t)t;
+    return make_uint2(v, ex);
+}
+
+// The prefix sort's tables (one workgroup of 256, after the first pass's histogram read; t =
+// tile = class): class starts in the full order P (class 0: the keys below 1.0; tiles 1..255:
+// their counts; class 256: the rest) and in the kept subset, the placement delta, the kept count
+// (the element count of passes 1-3), and per tile the first position of its draw window that
+// was not sorted -- in the draw's positions, which hold the reference's culled entries (cn of
+// them at cpos, k_draw) besides the sorted ones.  Counters are cleared for the next frame.
+__device__ void prefix_tables(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, const PrefixDev &pre,
+                              const uint32_t *__restrict__ cnt, uint32_t n_max, uint32_t *s_w) {
+    __shared__ uint32_t s_above, s_low, s_k256;
+    __shared__ uint32_t s_P[kClasses + 1], s_L[kClasses], s_G[kClasses], s_gw[4];
+    const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
+    const uint2 vb = bins_scan(counts, bins, s_w, &s_above);  // (its barriers publish s_above)
+    uint32_t kept = 0;
+#pragma unroll
+    for (int k = 0; k < kPrefixCopies; ++k) {
+        kept += pre.counts[k * kClasses + t];
+        pre.counts[k * kClasses + t] = 0;
+    }
+    if (t < kPrefixCopies) {  // class 256 and the keys below 1.0
+        uint32_t a = pre.counts[t * kClasses + 256], b = pre.counts[kPrefixCopies * kClasses + t];
+        pre.counts[t * kClasses + 256] = 0;
+        pre.counts[kPrefixCopies * kClasses + t] = 0;
+#pragma unroll
+        for (int o = 1; o < kPrefixCopies; o <<= 1) {
+            a += __shfl_xor(a, o, 64);
+            b += __shfl_xor(b, o, 64);
+        }
+        if (t == 0) {
+            s_k256 = a;
+            s_low = b;
+        }
+    }
+    __syncthreads();
+    const uint32_t E = elem_count(n_max, cnt);
+    const uint32_t m = t == 0 ? s_low : vb.x;  // keys of class t
+    uint32_t tot_m, tot_k;
+    const uint32_t P = block_excl_scan_tot<4>(m, s_w, &tot_m);
+    const uint32_t off = block_excl_scan_tot<4>(kept, s_w, &tot_k);
+    const uint32_t m256 = E - tot_m, k256 = s_k256;
+    pre.delta[t] = (int32_t)(P - off);
+    s_P[t] = P;
+    s_L[t] = P + kept;
+    if (t == 0) {
+        pre.delta[256] = (int32_t)(tot_m - tot_k);
+        s_P[256] = tot_m;
+        s_P[257] = E;
+        s_L[256] = tot_m + k256;
+        pre.nsel[0] = tot_k + k256;
+        pre.nsel[1] = 0;
+        if (pre.h_slot) pre.h_slot[3] = tot_k + k256;
+    }
+    // G[c]: the first position not sorted at or after class c's start (E: none) -- a suffix min
+    // of each class's gap (its kept end, when it kept less than all)
+    const uint32_t gap256 = k256 < m256 ? tot_m + k256 : E;
+    uint32_t g = kept < m ? P + kept : E;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_down(g, o, 64);
+        if (lane + o < 64) g = min(g, u);
+    }
+    if (lane == 0) s_gw[wid] = g;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+        if (w > wid) g = min(g, s_gw[w]);
+    g = min(g, gap256);
+    s_G[t] = g;
+    if (t == 0) s_G[256] = gap256;
+    __syncthreads();
+    // tile t's draw window starts at its bins start (draw positions; culled entries at [cpos, cpos + cn))
+    const int V = (int)cnt[0];
+    const uint32_t cn = pre.clean ? 0u : (uint32_t)max(0, pre.n - V);
+    const uint32_t cpos = (uint32_t)min(max((int)E - (int)s_above, 0), (int)E);
+    const uint32_t p0 = vb.y;
+    const uint32_t q0 = p0 < cpos ? p0 : (p0 < cpos + cn ? cpos : p0 - cn);
+    uint32_t fi = 0xffffffffu;
+    if (q0 < E) {
+        int c = 0;  // the last class starting at or before q0
+#pragma unroll
+        for (int step = 256; step > 0; step >>= 1)
+            if (c + step <= 256 && s_P[c + step] <= q0) c += step;
+        const uint32_t fq = q0 >= s_L[c] ? q0 : s_G[c];
+        if (fq < E) fi = fq < cpos ? fq : fq + cn;
+    }
+    bins[kBinsLimit + t] = fi;
 }
 
 // One workgroup of 256 per digit (a small workgroup finds room on a CU beside the previous
@@ -246,11 +369,16 @@ __device__ void bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ 
 __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
-                                                   uint32_t *__restrict__ bins) {
+                                                   uint32_t *__restrict__ bins, PrefixDev pre, int prefix) {
     constexpr int kPer = 16;
     __shared__ uint32_t s_w[4];
     if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
-        bins_scan(tile_counts, bins, s_w);
+        if (prefix) {
+            prefix_tables(tile_counts, bins, pre, cnt, n_max, s_w);
+        } else {
+            __shared__ uint32_t s_above;
+            bins_scan(tile_counts, bins, s_w, &s_above);
+        }
         return;
     }
     const uint32_t nb = (elem_count(n_max, cnt) + tile - 1) / tile;
@@ -280,13 +408,16 @@ __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, 
 //   kPackOut (key, value) in, packed out: key's top byte | value (value < 2^24), into kout
 //   kPackIn  packed in (kin), value out (vout): the last pass of a frame sort, whose keys
 //            nobody reads (the draw needs the values and the bins only)
-constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2;
-template <int W, int FMT>
+//   kPlace   (key, value) in, value out at its position in the full order: the last pass of a
+//            frame's prefix sort (position in the subset + pre.delta[class of the key])
+// PREFIX: the first pass of a prefix sort -- only the keys at or below their class bound move
+constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2, kPlace = 3;
+template <int W, int FMT, bool PREFIX = false>
 __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
                                                       const uint32_t *__restrict__ hist, uint32_t nb,
-                                                      const uint32_t *__restrict__ row_total) {
+                                                      const uint32_t *__restrict__ row_total, PrefixDev pre) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
@@ -298,8 +429,13 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     __shared__ uint32_t s_wave[kWaves];
     __shared__ uint32_t s_keys[kTile];
     __shared__ uint32_t s_vals[FMT == kPackIn ? 1 : kTile];
+    __shared__ int32_t s_cls[(PREFIX || FMT == kPlace) ? kClasses : 1];  // class bounds / placement deltas
+    __shared__ uint32_t s_tile_n;
 
     for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    if (PREFIX || FMT == kPlace)
+        for (int i = threadIdx.x; i < kClasses; i += kThreads)
+            s_cls[i] = PREFIX ? (int32_t)pre.theta[i] : pre.delta[i];
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t tile0 = tile * (uint32_t)kTile;
@@ -328,10 +464,16 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     //      issued back to back (one LDS round trip, not one per item);
     //   3. peers fetch their leader's returned value (ds_bpermute).
     uint32_t rank[kItems], lead[kItems], old[kItems];
+    uint32_t keepm = 0;  // PREFIX: bit k = item k is kept
+    if (PREFIX) {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if (base + k * 64 < n && kk[k] <= (uint32_t)s_cls[key_class(kk[k])]) keepm |= 1u << k;
+    }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
-        const bool valid = idx < n;
+        const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
         const uint32_t d = (kk[k] >> shift) & 0xffu;
         const uint64_t m = match_digit(d, __ballot(valid));
         rank[k] = count_below(m);
@@ -341,7 +483,8 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
-        if (idx < n && lead[k] == (uint32_t)lane)
+        const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
+        if (valid && lead[k] == (uint32_t)lane)
             old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
     }
 #pragma unroll
@@ -360,8 +503,10 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
                 tot += c;
             }
         }
-        const uint32_t start = block_excl_scan<W>(tot, s_wave);
+        uint32_t tile_kept;
+        const uint32_t start = block_excl_scan_tot<W>(tot, s_wave, &tile_kept);
         const uint32_t gdig = block_excl_scan<W>(dig ? row_total[d] : 0u, s_wave);  // digit base, whole array
+        if (PREFIX && threadIdx.x == 0) s_tile_n = tile_kept;
         if (dig) {
             s_start[d] = start;
             s_gbase[d] = (int32_t)(gdig + hist[(size_t)d * nb + tile]) - (int32_t)start;
@@ -371,7 +516,8 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const uint32_t idx = base + k * 64;
-        if (idx < n) {
+        const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
+        if (valid) {
             const uint32_t d = (kk[k] >> shift) & 0xffu;
             const uint32_t pos = s_start[d] + s_cnt[wid][d] + rank[k];
             s_keys[pos] = kk[k];
@@ -379,7 +525,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         }
     }
     __syncthreads();
-    const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
+    const uint32_t tile_n = PREFIX ? s_tile_n : min((uint32_t)kTile, n - tile0);
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
         const uint32_t d = (key >> shift) & 0xffu;
@@ -387,11 +533,74 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         if (FMT == kPairs) {
             kout[o] = key;
             vout[o] = s_vals[i];
+        } else if (FMT == kPlace) {
+            vout[(uint32_t)((int32_t)o + s_cls[key_class(key)])] = s_vals[i];
         } else if (FMT == kPackOut) {
             kout[o] = (key & 0xff000000u) | s_vals[i];
         } else {
             vout[o] = key & 0x00ffffffu;
         }
+    }
+}
+
+// The prefix sort's sampled histogram: key j * kPrefixSample of the frame's emitted keys goes
+// to copy j % kPrefixHistCopies (one thread per sample; the grid covers the capacity)
+__global__ __launch_bounds__(256) void k_prefix_sample(const uint32_t *__restrict__ keys, uint32_t n_max,
+                                                       const uint32_t *__restrict__ cnt, PrefixDev pre) {
+    const uint32_t n = elem_count(n_max, cnt);
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if ((uint64_t)j * kPrefixSample >= n) return;
+    const uint32_t key = keys[(size_t)j * kPrefixSample];
+    const uint32_t c = key_class(key);
+    if (c < 256u)
+        atomicAdd(&pre.hist[((size_t)(j % kPrefixHistCopies) * 256 + c) * kPrefixBuckets + prefix_bucket(class_hi(c) - key)],
+                  1u);
+}
+
+// The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
+// [8j, 8j + 8) of every copy): walking the sampled histogram from the largest distance (the
+// front of the list) down, the bucket where the count reaches target / kPrefixSample sets
+// theta = the class bound - that bucket's smallest distance; a class sampled less keeps every
+// key.  The histogram is cleared for the next frame.
+__global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
+    constexpr int kB = kPrefixBuckets / 256;  // buckets per thread (8)
+    __shared__ uint32_t s_w[4];
+    const uint32_t c = blockIdx.x, j = threadIdx.x;
+    uint32_t v[kB] = {};
+#pragma unroll
+    for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
+        uint4 *h = reinterpret_cast<uint4 *>(pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets + kB * j);
+        const uint4 q0 = h[0], q1 = h[1];
+        h[0] = make_uint4(0, 0, 0, 0);
+        h[1] = make_uint4(0, 0, 0, 0);
+        v[0] += q0.x; v[1] += q0.y; v[2] += q0.z; v[3] += q0.w;
+        v[4] += q1.x; v[5] += q1.y; v[6] += q1.z; v[7] += q1.w;
+    }
+    uint32_t a = 0;
+#pragma unroll
+    for (int k = 0; k < kB; ++k) a += v[k];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_tot<4>(a, s_w, &tot);
+    const uint32_t above = tot - ex - a;  // samples in the buckets of the higher threads
+    const uint32_t tgt = (pre.target + kPrefixSample - 1) / kPrefixSample;
+    const uint32_t hi = class_hi(c);
+    if (c == 0 && j == 0) pre.theta[256] = 0xffffffffu;  // class 256 is kept whole
+    if (pre.target == 0 || tot < tgt) {
+        if (j == 0) pre.theta[c] = hi - 1u;  // the whole class
+        return;
+    }
+    if (above < tgt && above + a >= tgt) {
+        uint32_t cum = above, b = 0;
+        bool found = false;
+#pragma unroll
+        for (int k = kB - 1; k >= 0; --k) {
+            cum += v[k];
+            if (!found && cum >= tgt) {
+                b = kB * j + (uint32_t)k;
+                found = true;
+            }
+        }
+        pre.theta[c] = hi - prefix_bucket_dmin(b);
     }
 }
 
@@ -448,7 +657,12 @@ void sort_free(SortScratch &sc) {
 }
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
-               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out) {
+               const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out,
+               const PrefixDev *pre) {
+    if (pre && (!bins || !dev_count)) {
+        err = "radix sort: a prefix sort needs bins and a device count";
+        return GS_ERR_INVALID;
+    }
     if (((n <= 1 && !dev_count) || n < 1) && !bins) {  // nothing to sort; the events still mark the call
         if (start) (void)hipEventRecord(start, s);
         if (stop) (void)hipEventRecord(stop, s);
@@ -464,44 +678,66 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
         if (start) (void)hipEventRecord(start, s);
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
-                           tile_counts, bins);
+                           tile_counts, bins, PrefixDev{}, 0);
         if (stop) (void)hipEventRecord(stop, s);
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
     }
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
+    const PrefixDev pd = pre ? *pre : PrefixDev{};
+    if (pre) {  // the class bounds from a sample of the keys
+        const uint32_t ns = (uint32_t)((n + kPrefixSample - 1) / kPrefixSample);
+        hipExtLaunchKernelGGL(k_prefix_sample, dim3(std::max<uint32_t>((ns + 255) / 256, 1)), dim3(256), 0, s, start,
+                              nullptr, 0, keys, (uint32_t)n, dev_count, pd);
+        hipLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, pd);
+        start = nullptr;
+    }
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
         const bool big = pass == 0;
         const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
         const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // tiles of this pass = hist row stride
+        // a prefix sort's passes 1-3 run on the kept keys (their count on the device)
+        const uint32_t *cnt = pre && pass > 0 ? pre->nsel : dev_count;
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
-        if (big && bins)
+        if (big && pre)
+            hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
+                                  0, kin, (uint32_t)n, cnt, shift, sc.hist, nb, tile_counts, pd);
+        else if (big && bins)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)n, dev_count, shift, sc.hist, nb, tile_counts);
+                                  kin, (uint32_t)n, cnt, shift, sc.hist, nb, tile_counts, pd);
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
+                                  kin, (uint32_t)n, cnt, shift, sc.hist, nb, nullptr, pd);
         else
             hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)n, dev_count, shift, sc.hist, nb, nullptr);
-        const bool with_bins = bins && pass == 3;  // one more workgroup scans the tile counts
+                                  0, kin, (uint32_t)n, cnt, shift, sc.hist, nb, nullptr, pd);
+        // one more workgroup scans the tile counts: in the last pass, or (prefix sort) in the
+        // first, with the class tables passes 1-3 need
+        const bool with_bins = bins && (pre ? pass == 0 : pass == 3);
         hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
-                           dev_count, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr);
-        // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only
-        const int fmt = keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
-        if (big)
+                           cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pre && pass == 0 ? 1 : 0);
+        // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
+        // a prefix sort moves pairs and places the values in its last pass
+        const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
+        if (big && pre)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+        else if (big)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
-                                  kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+                                  kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (fmt == kPairs)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
-                                  0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+                                  0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+        else if (fmt == kPlace)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
+                                  0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (fmt == kPackOut)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackOut>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackIn>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, shift, sc.hist, nb, sc.row_total);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

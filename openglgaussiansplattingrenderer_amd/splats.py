@@ -53,6 +53,21 @@ class Context:
         (throughput +1-2 % at C3); 1 runs frames one after the other"""
         check(lib().gs_ctx_set_lanes(self.handle, int(lanes)), self.handle)
 
+    def set_sort_prefix(self, target: int = -1) -> int:
+        """prefix sort of frames enqueued without a round trip (gs_ctx_set_sort_prefix): every
+        tile list sorted at least `target` entries deep (0: always the full sort; < 0: leave it);
+        returns the current target"""
+        cur = ctypes.c_int()
+        check(lib().gs_ctx_set_sort_prefix(self.handle, int(target), ctypes.byref(cur)), self.handle)
+        return cur.value
+
+    def prefix_stats(self, reset: bool = False) -> dict:
+        """gs_prefix_stats: frames prefix-sorted, of them rendered again, entries kept / entries of
+        the newest retired prefix-sorted frame"""
+        a = np.zeros(4, np.uint64)
+        check(lib().gs_prefix_stats(self.handle, ptr(a), int(reset)), self.handle)
+        return dict(frames=int(a[0]), redone=int(a[1]), kept=int(a[2]), entries=int(a[3]))
+
     def timing_reset(self):
         check(lib().gs_timing_reset(self.handle), self.handle)
 
