@@ -95,6 +95,7 @@ struct gs_ctx {
         const void *draw_out = nullptr;
         bool drawn = false, draw_stats = false;
         bool prefix = false;  // prefix-sorted: its blend may flag a miss (ring word 2)
+        uint32_t cap_sel = 0;  // prefix-sorted: the kept entries its sort passes 1-3 could hold
     };
     Slot slot[kRing];
     hipEvent_t ev[kRing][kEv] = {};
@@ -332,15 +333,15 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             // a prefix-sorted frame whose blend reached an unsorted position: render it again
             // (full sort) and sort deeper from now on
             const bool miss = sl.prefix && ctx->h_ring[4 * k + 2] != 0;
-            if (miss) {
-                ctx->prefix_redo += 1;
-                ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
-            }
-            if (V + D > sl.cap || miss) return handle_overflow(ctx);
+            // ... or that kept more entries than its sort passes could hold (sized from earlier frames)
+            const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
             if (sl.prefix) {
                 ctx->prefix_kept = ctx->h_ring[4 * k + 3];
                 ctx->prefix_E = (uint64_t)(V + D);
             }
+            if (miss) ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
+            if (miss || full) ctx->prefix_redo += 1;
+            if (V + D > sl.cap || miss || full) return handle_overflow(ctx);
             ctx->V = V;
             ctx->D = D;
             ctx->E = V + D;
@@ -840,11 +841,11 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     return GS_OK;
 }
 
-int enqueue_emit(gs_ctx *ctx) {
+int enqueue_emit(gs_ctx *ctx, uint32_t *prefix_hist = nullptr) {
     ctx->L->keys_sorted = true;  // emission order, as gs_frame_read shows it before gs_sort
     ctx->L->vals_partial = false;
     gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap, fev(ctx, 2),
-                    fev(ctx, 3));
+                    fev(ctx, 3), prefix_hist);
     GS_HIP(ctx, hipGetLastError());
     return GS_OK;
 }
@@ -994,6 +995,13 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.counts = pd.theta + gs::kClasses;
         pd.nsel = pd.counts + (size_t)gs::kPrefixCopies * (gs::kClasses + 1);
         pd.delta = (int32_t *)(pd.nsel + 2);
+        pd.cls = (uint32_t *)(pd.delta + gs::kClasses);
+        // passes 1-3 sized for the kept count of the newest retired prefix-sorted frame + 25 %
+        // (+ 64Ki); the first one: every entry
+        const int64_t cap_e = ctx->L->e_cap;
+        pd.cap_sel = (uint32_t)(ctx->prefix_kept ? std::min<int64_t>(cap_e, (int64_t)ctx->prefix_kept * 5 / 4 + 65536)
+                                                 : cap_e);
+        sl.cap_sel = pd.cap_sel;
         pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
         pd.target = (uint32_t)ctx->prefix_target;
         pd.n = scene->n;
@@ -1002,7 +1010,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         ctx->prefix_frames += 1;
     }
     int rc;
-    if ((rc = enqueue_emit(ctx)) ||
+    if ((rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr)) ||
         (rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr)))
         return rc;
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,

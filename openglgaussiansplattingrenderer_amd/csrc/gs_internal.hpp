@@ -53,21 +53,25 @@ constexpr int kBinCountWords = 260;  // counts of k_bins_count: [0, 256) tiles, 
 // prefix of every list (gs_sort.hip, "prefix sort"):
 //   * key classes: c = t for keys in [t, t+1) (t = 0..255, the tile lists of the bins), and
 //     c = 256 for every other bit pattern (>= 256, inf, NaN, negative), always kept whole;
-//   * k_prefix_sample adds one emitted key in kPrefixSample to a per-class histogram of the
+//   * k_emit adds one emitted key in kPrefixSample to a per-class histogram of the
 //     distance d = bits(t + 1) - key (floating-point buckets: 5-bit exponent, 6-bit mantissa;
-//     kPrefixHistCopies copies, so the few hot buckets of a deep list do not serialise);
+//     kPrefixHistCopies copies and consecutive buckets 1 KiB apart, so the hot buckets of a
+//     deep list do not serialise on one cache line);
 //   * k_prefix_select picks per class the largest key bound whose sampled count reaches
 //     target / kPrefixSample (or keeps the class whole);
 //   * the first sort pass keeps the keys at or below their class bound (stable), the other
 //     passes sort that subset, and the last one writes each value at its position in the full
 //     sorted order (class start in the full order - class start in the subset);
-//   * the bins workgroup stores per tile the first position of its draw window that was not
-//     sorted (bins[kBinsLimit + t]); a sub-block that reaches it unsaturated flags the frame
-//     (pinned ring word 2), which is then rendered again with the full sort.
+//   * the first pass's scan adds one workgroup for the class tables (kept count, placement),
+//     the last pass's bins workgroup stores per tile the first position of its draw window
+//     that was not sorted (bins[kBinsLimit + t]); a sub-block that reaches it unsaturated flags
+//     the frame (pinned ring word 2 = 1), which is then rendered again with the full sort.
 constexpr int kClasses = 257;
 constexpr int kPrefixBuckets = 2048;
-constexpr int kPrefixSample = 64;
-constexpr int kPrefixHistCopies = 8;
+constexpr int kPrefixSample = 128;
+constexpr int kPrefixHistCopies = 2;
+// word of bucket b in its class's histogram: consecutive buckets on different cache lines
+__host__ __device__ constexpr uint32_t prefix_slot(uint32_t b) { return (b & 7u) * (kPrefixBuckets / 8) + (b >> 3); }
 constexpr int kPrefixCopies = 16;  // selected-count copies (spread same-address atomics)
 struct PrefixDev {
     uint32_t *hist;    // [kPrefixHistCopies][256][kPrefixBuckets] sampled counts (zero between frames)
@@ -75,6 +79,9 @@ struct PrefixDev {
     uint32_t *counts;  // [kPrefixCopies][kClasses] kept per class, then [kPrefixCopies] keys < 1.0 (zero between frames)
     uint32_t *nsel;    // [2]: kept keys, 0 (the element count of passes 1-3)
     int32_t *delta;    // [kClasses]: full-order start - subset start of each class
+    uint32_t *cls;     // [kClasses + 1] class starts in the full order (then E), [kClasses] ends of their kept keys
+    uint32_t cap_sel;  // elements passes 1-3 are sized for (more kept: the host renders the frame again)
+    const uint32_t *frame_count;  // the frame's device (V, D) (set by sort_pairs)
     uint32_t *h_slot;  // mapped pinned ring slot of the frame: [3] = kept keys (diagnostics), or null
     uint32_t target;   // entries per class to keep at least
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
@@ -105,7 +112,9 @@ __host__ __device__ inline uint32_t prefix_bucket_dmin(uint32_t b) {
     const uint32_t e = b >> 6, m = 64u | (b & 63u);
     return e >= 6 ? m << (e - 6) : m >> (6 - e);
 }
-constexpr size_t kPrefixWords = (size_t)kPrefixHistCopies * 256 * kPrefixBuckets + kClasses + (size_t)kPrefixCopies * (kClasses + 1) + 2 + kClasses;
+constexpr size_t kPrefixWords =
+    (size_t)kPrefixHistCopies * 256 * kPrefixBuckets + kClasses + (size_t)kPrefixCopies * (kClasses + 1) + 2 + kClasses +
+    (2 * kClasses + 1);
 
 // Per-frame uniforms of the preprocess kernel (preprocess.glsl:18-37)
 struct PreParams {
@@ -195,8 +204,9 @@ int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block s
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);
 bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preprocess) fits this frame
+// prefix_hist != null: also sample the emitted keys into the prefix sort's histogram
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
-                 hipEvent_t start, hipEvent_t stop);
+                 hipEvent_t start, hipEvent_t stop, uint32_t *prefix_hist = nullptr);
 // E entries, or min(E, dev_count[0] + dev_count[1]) when dev_count is given; counts must be
 // zero on entry and are left zero
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,

@@ -412,7 +412,8 @@ __device__ __forceinline__ void wave_sync_lds() {
 // known on the host; the host detects the overflow from the totals and renders again).
 template <bool PACK>
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
-                                                 uint32_t *__restrict__ vals, uint32_t cap) {
+                                                 uint32_t *__restrict__ vals, uint32_t cap,
+                                                 uint32_t *__restrict__ phist) {
     __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ uint32_t s_incl[kBlock / 64][64];  // per wave: inclusive duplicate counts
     __shared__ int4 s_rec[kBlock / 64][64];       // per wave: the lanes' preprocess records
@@ -490,6 +491,27 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
         }
         carry_m += t0;
         carry_d += t1;
+    }
+    // prefix sort (gs_internal.hpp): the emitted keys at positions j * kPrefixSample of this
+    // workgroup's two output ranges go to the sampled histogram (copy j % kPrefixHistCopies) --
+    // after the loop, so no load of it waits behind these atomics
+    if (phist) {
+        __threadfence_block();
+        __syncthreads();  // the workgroup's own key stores are visible to it
+        const uint32_t r0[2] = {off.x, V + off.y}, r1[2] = {carry_m, V + carry_d};
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t j = (r0[r] + kPrefixSample - 1) / kPrefixSample + threadIdx.x;
+            const uint32_t p = j * kPrefixSample;
+            if (p < r1[r] && p < cap) {
+                const uint32_t key = keys[p];
+                const uint32_t c = key_class(key);
+                if (c < 256u)
+                    atomicAdd(&phist[((size_t)(j % kPrefixHistCopies) * 256 + c) * kPrefixBuckets +
+                                     prefix_slot(prefix_bucket(class_hi(c) - key))],
+                              1u);
+            }
+        }
     }
 }
 
@@ -1128,10 +1150,10 @@ void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEv
 }
 
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
-                 hipEvent_t start, hipEvent_t stop) {
+                 hipEvent_t start, hipEvent_t stop, uint32_t *prefix_hist) {
     const dim3 grid(std::max(preprocess_blocks(n), 1));
-    if (packed) hipExtLaunchKernelGGL(k_emit<true>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap);
-    else hipExtLaunchKernelGGL(k_emit<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap);
+    if (packed) hipExtLaunchKernelGGL(k_emit<true>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, prefix_hist);
+    else hipExtLaunchKernelGGL(k_emit<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, prefix_hist);
 }
 
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,

@@ -274,23 +274,22 @@ __device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__
     return make_uint2(v, ex);
 }
 
-// The prefix sort's tables (one workgroup of 256, after the first pass's histogram read; t =
-// tile = class): class starts in the full order P (class 0: the keys below 1.0; tiles 1..255:
-// their counts; class 256: the rest) and in the kept subset, the placement delta, the kept count
-// (the element count of passes 1-3), and per tile the first position of its draw window that
-// was not sorted -- in the draw's positions, which hold the reference's culled entries (cn of
-// them at cpos, k_draw) besides the sorted ones.  Counters are cleared for the next frame.
-__device__ void prefix_tables(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, const PrefixDev &pre,
+// The prefix sort's class tables (one workgroup of 256 in the first pass's scan, after its
+// histogram read; t = tile = class): class starts in the full order P (class 0: the keys below
+// 1.0; tiles 1..255: their counts; class 256: the rest) and in the kept subset, the placement
+// delta, the kept count (the element count of passes 1-3; above their capacity the frame is
+// flagged).  The kept counters are cleared for the next frame (the tile counts stay for the
+// bins workgroup of the last pass).
+__device__ void prefix_counts(const uint32_t *__restrict__ tile_counts, const PrefixDev &pre,
                               const uint32_t *__restrict__ cnt, uint32_t n_max, uint32_t *s_w) {
-    __shared__ uint32_t s_above, s_low, s_k256;
-    __shared__ uint32_t s_P[kClasses + 1], s_L[kClasses], s_G[kClasses], s_gw[4];
-    const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
-    const uint2 vb = bins_scan(counts, bins, s_w, &s_above);  // (its barriers publish s_above)
-    uint32_t kept = 0;
+    __shared__ uint32_t s_low, s_k256;
+    const int t = threadIdx.x;
+    uint32_t kept = 0, v = 0;
 #pragma unroll
     for (int k = 0; k < kPrefixCopies; ++k) {
         kept += pre.counts[k * kClasses + t];
         pre.counts[k * kClasses + t] = 0;
+        v += tile_counts[k * kRadix + t];
     }
     if (t < kPrefixCopies) {  // class 256 and the keys below 1.0
         uint32_t a = pre.counts[t * kClasses + 256], b = pre.counts[kPrefixCopies * kClasses + t];
@@ -308,27 +307,49 @@ __device__ void prefix_tables(uint32_t *__restrict__ counts, uint32_t *__restric
     }
     __syncthreads();
     const uint32_t E = elem_count(n_max, cnt);
-    const uint32_t m = t == 0 ? s_low : vb.x;  // keys of class t
+    const uint32_t m = t == 0 ? s_low : v;  // keys of class t
     uint32_t tot_m, tot_k;
     const uint32_t P = block_excl_scan_tot<4>(m, s_w, &tot_m);
     const uint32_t off = block_excl_scan_tot<4>(kept, s_w, &tot_k);
-    const uint32_t m256 = E - tot_m, k256 = s_k256;
     pre.delta[t] = (int32_t)(P - off);
-    s_P[t] = P;
-    s_L[t] = P + kept;
+    pre.cls[t] = P;
+    pre.cls[kClasses + 1 + t] = P + kept;
     if (t == 0) {
+        const uint32_t nsel = tot_k + s_k256;
         pre.delta[256] = (int32_t)(tot_m - tot_k);
-        s_P[256] = tot_m;
-        s_P[257] = E;
-        s_L[256] = tot_m + k256;
-        pre.nsel[0] = tot_k + k256;
+        pre.cls[256] = tot_m;
+        pre.cls[257] = E;
+        pre.cls[kClasses + 1 + 256] = tot_m + s_k256;
+        pre.nsel[0] = nsel;
         pre.nsel[1] = 0;
-        if (pre.h_slot) pre.h_slot[3] = tot_k + k256;
+        if (pre.h_slot) pre.h_slot[3] = nsel;  // (above cap_sel: passes 1-3 cannot hold them, the host renders again)
+    }
+}
+
+// The prefix sort's draw limits (the bins workgroup of the last pass): the bins, then per tile
+// the first position of its draw window that was not sorted -- in the draw's positions, which
+// hold the reference's culled entries (cn of them at cpos, k_draw) besides the sorted ones;
+// 0xffffffff: none.
+__device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, const PrefixDev &pre,
+                              const uint32_t *__restrict__ cnt, uint32_t *s_w) {
+    __shared__ uint32_t s_above;
+    __shared__ uint32_t s_P[kClasses + 1], s_L[kClasses], s_G[kClasses], s_gw[4];
+    const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
+    const uint2 vb = bins_scan(counts, bins, s_w, &s_above);  // (its barriers publish s_above)
+    const uint32_t P = pre.cls[t], L = pre.cls[kClasses + 1 + t];
+    const uint32_t P256 = pre.cls[256], E = pre.cls[257], L256 = pre.cls[kClasses + 1 + 256];
+    const uint32_t Pn = t < 255 ? pre.cls[t + 1] : P256;  // the next class's start
+    s_P[t] = P;
+    s_L[t] = L;
+    if (t == 0) {
+        s_P[256] = P256;
+        s_P[257] = E;
+        s_L[256] = L256;
     }
     // G[c]: the first position not sorted at or after class c's start (E: none) -- a suffix min
     // of each class's gap (its kept end, when it kept less than all)
-    const uint32_t gap256 = k256 < m256 ? tot_m + k256 : E;
-    uint32_t g = kept < m ? P + kept : E;
+    const uint32_t gap256 = L256 < E ? L256 : E;
+    uint32_t g = L < Pn ? L : E;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t u = __shfl_down(g, o, 64);
@@ -373,8 +394,10 @@ __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, 
     constexpr int kPer = 16;
     __shared__ uint32_t s_w[4];
     if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
-        if (prefix) {
-            prefix_tables(tile_counts, bins, pre, cnt, n_max, s_w);
+        if (prefix == 1) {
+            prefix_counts(tile_counts, pre, cnt, n_max, s_w);
+        } else if (prefix == 2) {
+            prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w);
         } else {
             __shared__ uint32_t s_above;
             bins_scan(tile_counts, bins, s_w, &s_above);
@@ -543,20 +566,6 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     }
 }
 
-// The prefix sort's sampled histogram: key j * kPrefixSample of the frame's emitted keys goes
-// to copy j % kPrefixHistCopies (one thread per sample; the grid covers the capacity)
-__global__ __launch_bounds__(256) void k_prefix_sample(const uint32_t *__restrict__ keys, uint32_t n_max,
-                                                       const uint32_t *__restrict__ cnt, PrefixDev pre) {
-    const uint32_t n = elem_count(n_max, cnt);
-    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    if ((uint64_t)j * kPrefixSample >= n) return;
-    const uint32_t key = keys[(size_t)j * kPrefixSample];
-    const uint32_t c = key_class(key);
-    if (c < 256u)
-        atomicAdd(&pre.hist[((size_t)(j % kPrefixHistCopies) * 256 + c) * kPrefixBuckets + prefix_bucket(class_hi(c) - key)],
-                  1u);
-}
-
 // The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
 // [8j, 8j + 8) of every copy): walking the sampled histogram from the largest distance (the
 // front of the list) down, the bucket where the count reaches target / kPrefixSample sets
@@ -566,15 +575,16 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     constexpr int kB = kPrefixBuckets / 256;  // buckets per thread (8)
     __shared__ uint32_t s_w[4];
     const uint32_t c = blockIdx.x, j = threadIdx.x;
+    static_assert(kB == 8, "prefix_slot puts bucket 8j + k at word k * (kPrefixBuckets / 8) + j");
     uint32_t v[kB] = {};
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
-        uint4 *h = reinterpret_cast<uint4 *>(pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets + kB * j);
-        const uint4 q0 = h[0], q1 = h[1];
-        h[0] = make_uint4(0, 0, 0, 0);
-        h[1] = make_uint4(0, 0, 0, 0);
-        v[0] += q0.x; v[1] += q0.y; v[2] += q0.z; v[3] += q0.w;
-        v[4] += q1.x; v[5] += q1.y; v[6] += q1.z; v[7] += q1.w;
+        uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            v[k] += h[prefix_slot(kB * j + k)];
+            h[prefix_slot(kB * j + k)] = 0;
+        }
     }
     uint32_t a = 0;
 #pragma unroll
@@ -683,61 +693,62 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
     }
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
-    const PrefixDev pd = pre ? *pre : PrefixDev{};
-    if (pre) {  // the class bounds from a sample of the keys
-        const uint32_t ns = (uint32_t)((n + kPrefixSample - 1) / kPrefixSample);
-        hipExtLaunchKernelGGL(k_prefix_sample, dim3(std::max<uint32_t>((ns + 255) / 256, 1)), dim3(256), 0, s, start,
-                              nullptr, 0, keys, (uint32_t)n, dev_count, pd);
-        hipLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, pd);
+    PrefixDev pd = pre ? *pre : PrefixDev{};
+    pd.frame_count = dev_count;
+    const int64_t n_sub = pre ? std::min<int64_t>(n, pre->cap_sel) : n;  // passes 1-3 of a prefix sort
+    if (pre) {  // the class bounds from the keys the emission sampled
+        hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
         start = nullptr;
     }
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
         const bool big = pass == 0;
         const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
-        const uint32_t nb = (uint32_t)((n + tile - 1) / tile);  // tiles of this pass = hist row stride
-        // a prefix sort's passes 1-3 run on the kept keys (their count on the device)
+        // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
         const uint32_t *cnt = pre && pass > 0 ? pre->nsel : dev_count;
+        const int64_t np = pass > 0 ? n_sub : n;
+        const uint32_t nb = (uint32_t)((np + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         if (big && pre)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)n, cnt, shift, sc.hist, nb, tile_counts, pd);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd);
         else if (big && bins)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)n, cnt, shift, sc.hist, nb, tile_counts, pd);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd);
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)n, cnt, shift, sc.hist, nb, nullptr, pd);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd);
         else
             hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)n, cnt, shift, sc.hist, nb, nullptr, pd);
-        // one more workgroup scans the tile counts: in the last pass, or (prefix sort) in the
-        // first, with the class tables passes 1-3 need
-        const bool with_bins = bins && (pre ? pass == 0 : pass == 3);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)n,
-                           cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pre && pass == 0 ? 1 : 0);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd);
+        // one more workgroup scans the tile counts in the last pass (a prefix sort: with the draw
+        // limits; and one in the first pass makes the class tables passes 1-3 need)
+        const bool with_bins = bins && (pass == 3 || (pre && pass == 0));
+        const int pmode = !pre ? 0 : pass == 0 ? 1 : 2;
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)np,
+                           cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pmode);
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
         if (big && pre)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (big)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
-                                  kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (fmt == kPairs)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
-                                  0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (fmt == kPlace)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
-                                  0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else if (fmt == kPackOut)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackOut>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         else
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackIn>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)n, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
