@@ -19,6 +19,8 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace gs {
 
 namespace {
@@ -487,32 +489,65 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     //      issued back to back (one LDS round trip, not one per item);
     //   3. peers fetch their leader's returned value (ds_bpermute).
     uint32_t rank[kItems], lead[kItems], old[kItems];
-    uint32_t keepm = 0;  // PREFIX: bit k = item k is kept
+    uint32_t keepm = 0;  // PREFIX: bit k = item k is kept (after the compaction: k * 64 + lane < kept)
+    uint32_t nit = kItems;  // items holding elements (uniform)
     if (PREFIX) {
+        // The kept keys of the wave (about a fifth) move to the front of its 1024 slots, in
+        // (item, lane) order -- the order stability needs -- so only ceil(kept / 64) items are
+        // ranked.  (s_keys / s_vals are free until the block-level reorder below.)
+        uint32_t *ck = s_keys + wid * kWaveTile, *cv = s_vals + wid * kWaveTile;
+        uint32_t nk = 0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if (base + k * 64 < n && kk[k] <= (uint32_t)s_cls[key_class(kk[k])]) keepm |= 1u << k;
+        for (int k = 0; k < kItems; ++k) {
+            const bool keep = base + k * 64 < n && kk[k] <= (uint32_t)s_cls[key_class(kk[k])];
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const uint32_t slot = nk + count_below(m);
+                ck[slot] = kk[k];
+                cv[slot] = vv[k];
+            }
+            nk += (uint32_t)__popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        nit = (nk + 63) / 64;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t slot = (uint32_t)(k * 64 + lane);
+            if ((uint32_t)k < nit && slot < nk) {
+                kk[k] = ck[slot];
+                vv[k] = cv[slot];
+                keepm |= 1u << k;
+            }
+        }
     }
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t idx = base + k * 64;
-        const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
-        const uint32_t d = (kk[k] >> shift) & 0xffu;
-        const uint64_t m = match_digit(d, __ballot(valid));
-        rank[k] = count_below(m);
-        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
-        old[k] = valid ? (uint32_t)__popcll(m) : 0u;  // count, replaced by the atomic's result
-    }
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t idx = base + k * 64;
-        const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
-        if (valid && lead[k] == (uint32_t)lane)
-            old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    // the ranking of the first NI items (the others hold no element)
+#define GS_RANK_ITEMS(NI)                                                                             \
+    do {                                                                                              \
+        _Pragma("unroll") for (int k = 0; k < (NI); ++k) {                                            \
+            const uint32_t idx = base + k * 64;                                                       \
+            const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
+            const uint32_t d = (kk[k] >> shift) & 0xffu;                                              \
+            const uint64_t m = match_digit(d, __ballot(valid));                                       \
+            rank[k] = count_below(m);                                                                 \
+            lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;                          \
+            old[k] = valid ? (uint32_t)__popcll(m) : 0u; /* count, replaced by the atomic's result */ \
+        }                                                                                             \
+        _Pragma("unroll") for (int k = 0; k < (NI); ++k) {                                            \
+            const uint32_t idx = base + k * 64;                                                       \
+            const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
+            if (valid && lead[k] == (uint32_t)lane)                                                   \
+                old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);                    \
+        }                                                                                             \
+        _Pragma("unroll") for (int k = 0; k < (NI); ++k) rank[k] +=                                   \
+            (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);                 \
+    } while (0)
+    if (!PREFIX) GS_RANK_ITEMS(kItems);
+    else if (nit <= kItems / 4) GS_RANK_ITEMS(kItems / 4);  // uniform
+    else if (nit <= kItems / 2) GS_RANK_ITEMS(kItems / 2);
+    else GS_RANK_ITEMS(kItems);
+#undef GS_RANK_ITEMS
     __syncthreads();
     {
         const int d = threadIdx.x;  // one thread per digit (threads >= 256 contribute zeros)
