@@ -326,6 +326,12 @@ def main():
     local_s = t1 - t0
     elapsed = max_over_ranks(pg, local_s)
     tm_draw = ctx.timing_read()
+    ps = ctx.prefix_stats()  # the prefix sort over the timed and untimed frames (gs_prefix_stats)
+    prefix = {"target": ctx.set_sort_prefix(), "frames": ps["frames"], "rendered_again": ps["redone"],
+              "kept_entries": ps["kept"], "entries": ps["entries"],
+              "kept_frac": round(ps["kept"] / max(1, ps["entries"]), 4),
+              "source": "gs_prefix_stats: each tile list sorted >= target entries deep; a frame whose blend "
+                        "reaches an unsorted position is rendered again with the full sort"}
     host = {"enqueue_ms_per_frame": round((tm_draw["ms_host_render"] - tm_draw["ms_host_wait"]) /
                                           max(1, tm_draw["host_renders"]), 4),
             "blocked_ms_per_frame": round(tm_draw["ms_host_wait"] / max(1, tm_draw["host_renders"]), 4),
@@ -418,6 +424,7 @@ def main():
                       "frames_in_flight": args.lanes,
                       "serial_ms_per_frame": round(serial_ms, 4),
                       "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
+                      "prefix_sort": prefix,
                       "frame_hbm_frac_algorithmic": round(frame_frac, 4)},
             "host": host,
             "ranks": ranks,
