@@ -199,20 +199,34 @@ def load_pmc(kernel: str, field: str = "hbm_bytes_per_launch"):
 SIMDS = 1024            # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 CLOCK_GHZ = 2.4         # peak engine clock
 VALU_CYC = 2            # cycles per wave64 VALU instruction at full issue (v_fma_f32 row)
+SHADER_ENGINES = 32     # SQ_BUSY_CYCLES is summed over them
 
 
 def issue_ceiling(kernel: str, launch_ms: float):
-    """The blend is bound by instruction issue, not HBM: its VALU instructions per launch (SQ
-    pass) at one wave64 VALU per SIMD every 2 cycles on all 1024 SIMDs at 2.4 GHz give the
-    issue ceiling; frac = ceiling / measured launch time."""
+    """The blend is bound by vector-instruction issue, not HBM.  Two views from the SQ pass
+    (profiles/pmc_summary.json, same collection as the traffic):
+      * naive: SQ_INSTS_VALU at one wave64 VALU per SIMD every 2 cycles at 2.4 GHz -- a lower
+        bound on the issue time, since most of the blend's instructions cost more than v_fma_f32
+        (tools/micro/valu_cost.hip: v_readlane / v_cmp to an SGPR 1.7x, v_mbcnt / v_cndmask /
+        v_med3 1.5x, packed fp32 1.8x, v_exp_f32 2.8x at 6 waves per SIMD);
+      * vector-ALU occupancy: SQ_ACTIVE_INST_VALU (quad-cycles) x 4 over the SIMD-cycles of the
+        dispatch (SQ_BUSY_CYCLES / 32 shader engines x 1024 SIMDs): the fraction of the kernel's
+        time its VALU instructions occupy the SIMDs at one quad-cycle each."""
     sq = load_pmc(kernel, "sq")
     if not sq or not sq.get("SQ_INSTS_VALU"):
         return None
     v = float(sq["SQ_INSTS_VALU"])
     ceil_ms = v * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e9) * 1e3
-    return {"valu_insts_per_launch": v, "salu_insts_per_launch": sq.get("SQ_INSTS_SALU"),
-            "ceiling_ms": round(ceil_ms, 4), "frac": round(ceil_ms / launch_ms, 4),
-            "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cyc / (1024 SIMDs x 2.4 GHz)"}
+    out = {"valu_insts_per_launch": v, "salu_insts_per_launch": sq.get("SQ_INSTS_SALU"),
+           "ceiling_ms": round(ceil_ms, 4), "frac": round(ceil_ms / launch_ms, 4),
+           "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cyc / (1024 SIMDs x 2.4 GHz)"}
+    act, busy = sq.get("SQ_ACTIVE_INST_VALU"), sq.get("SQ_BUSY_CYCLES")
+    if act and busy:
+        simd_cycles = float(busy) / SHADER_ENGINES * SIMDS
+        out["valu_occupancy"] = round(4.0 * float(act) / simd_cycles, 4)
+        out["valu_occupancy_source"] = ("SQ_ACTIVE_INST_VALU x 4 / (SQ_BUSY_CYCLES / 32 x 1024): SIMD time the "
+                                        "blend's VALU instructions occupy, one quad-cycle each")
+    return out
 
 
 def main():
