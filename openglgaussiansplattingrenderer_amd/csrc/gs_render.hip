@@ -696,6 +696,9 @@ struct alignas(16) SurvRgb {
 };
 static_assert(offsetof(SplatDraw, thr) == offsetof(SurvData, thr), "SurvData mirrors SplatDraw");
 
+#ifndef GS_DRAW_BATCH
+#define GS_DRAW_BATCH 32
+#endif
 template <bool FAST_EXP, bool STATS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
@@ -710,6 +713,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
     __shared__ float s_epow[256 + 64];
     __shared__ uint8_t s_epix[256 + 64];
+    // box survivors queued in list order until a batch is blended (kBatch <= 64; <= 127 queued)
+    __shared__ uint32_t s_q[128];
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
@@ -857,19 +862,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // blocks with few pixels in the image start sparse
     if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) go_sparse();
 
-    // The list streams through a four-stage pipeline, one 64-entry chunk per step; chunk c:
-    //   step c-3: index load (coalesced)            step c-2: box gather
-    //   step c-1: box test, splat-data gather       step c:   exact cull + blend
-    // Each stage's registers live one step, so two slots (ping-pong, unrolled) hold them.
-    // Every global load is issued with the full exec mask and no branch around it, and no
-    // register with a pending load is ever copied: a load under a divergent branch or such a
-    // copy makes the compiler wait for all outstanding loads (vmcnt is in-order) and the
-    // pipeline collapses to one memory latency per step.
+    // The list streams through a three-stage pipeline, one 64-entry chunk per step; chunk c:
+    //   step c-2: index load (coalesced)   step c-1: box gather   step c: box test
+    // and the chunk's box survivors join a queue in LDS (list order).  Once kBatch are queued,
+    // the first up to 64 become a batch: one survivor per lane gathers its splat data, and the
+    // next step culls (exact ellipse test, all lanes busy) and blends the batch.  Each stage's
+    // registers live one step, so two slots (ping-pong, unrolled) hold them.  Every global load
+    // is issued with the full exec mask and no branch around it, and no register with a pending
+    // load is ever copied: a load under a divergent branch or such a copy makes the compiler
+    // wait for all outstanding loads (vmcnt is in-order) and the pipeline collapses to one
+    // memory latency per step.
+    constexpr uint32_t kBatch = GS_DRAW_BATCH;
     uint32_t Vi[2], Vb[2];      // indices: as loaded / riding with the box gather
     uint2 Bx[2];                // boxes (int16 pixel bounds, pack_box)
-    uint64_t K[2];              // survivors of the box test (then of the exact cull)
-    SurvData Dd[2];             // survivor data (lane-held; other lanes hold copies)
-    SurvRgb Dc[2];              // survivor colour
+    SurvData Dd;                // the batch's survivor data (lane j: survivor j)
+    SurvRgb Dc;                 // ... colour
+    uint64_t bk = 0;            // the batch's lanes (uniform)
+    uint32_t qn = 0;            // survivors queued (uniform)
+    bool inflight = false;      // a batch's data gather is in flight (uniform)
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -889,19 +899,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         vb = v;
         bx = *at(cullbox, v << 3);
     };
-    auto test_and_gather = [&](int cbase, uint32_t v, const uint2 &bx, uint64_t &keep, SurvData &d,
-                               SurvRgb &c) {
+    // box test of a chunk; its survivors join the queue
+    auto test_and_queue = [&](int cbase, uint32_t v, const uint2 &bx) __attribute__((always_inline)) {
         // bitwise, not short-circuit: no branch around the compares
         const bool in = (cbase + lane < end) &
                         (!cull | (((bx.x & 0xffffu) <= irx1) & ((bx.x >> 16) >= irx0) & ((bx.y & 0xffffu) <= iry1) &
                                   ((bx.y >> 16) >= iry0)));
-        keep = ballot(in);
-        // survivors gather their splat; the other lanes re-read the first survivor's (same lines)
-        const uint32_t first = keep ? (uint32_t)__builtin_amdgcn_readlane((int)v, (int)__builtin_ctzll(keep)) : 0u;
-        const uint32_t idx = in ? v : first;
+        const uint64_t m = ballot(in);
+        if (in) s_q[below(m, qn)] = v;
+        qn += (uint32_t)__popcll(m);
+    };
+    // the first up to 64 queued survivors become the batch: lane j gathers survivor j's splat
+    // (lanes past the batch re-read its last survivor: same lines); the rest of the queue moves up
+    auto issue_batch = [&]() __attribute__((always_inline)) {
+        wave_lds_sync();
+        const uint32_t bn = min(qn, 64u);
+        const uint32_t id = s_q[min((uint32_t)lane, bn - 1u)];
         // the 7 used floats of the SplatDraw record and rgb of the colour
-        d = *at(reinterpret_cast<const SurvData *>(sd), idx << 5);
-        c = *at(reinterpret_cast<const SurvRgb *>(colour), idx << 4);
+        Dd = *at(reinterpret_cast<const SurvData *>(sd), id << 5);
+        Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
+        bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
+        if (qn > 64u) {  // uniform, rare
+            const uint32_t r = s_q[64 + lane];
+            wave_lds_sync();
+            if ((uint32_t)lane < qn - 64u) s_q[lane] = r;
+        }
+        qn -= bn;
+        inflight = true;
     };
     // dense phase: every survivor's power at all 256 pixels, its blend events compacted into
     // LDS and run one per lane.  Returns true when the block turns sparse (keep: the chunk's
@@ -1064,34 +1088,34 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         }
     };
 
-    // prologue: chunk 0 box-gathered, chunk 1 index-loaded ... see the stage table above
+    // the batch in flight: exact cull and blend (its data arrived; uniform branches)
+    auto blend_batch = [&]() __attribute__((always_inline)) {
+        if (!sparse && blend_dense(bk, Dd, Dc)) go_sparse();
+        if (sparse) blend_sparse(bk, Dd, Dc);
+        inflight = false;
+    };
+    // prologue: chunk 0 index-loaded and box-gathered, chunk 1 index-loaded
     int base = start;
     if (base < end && !all_done) {  // uniform
         uint32_t v0;
         load_idx(base, v0);
         load_idx(base + 64, Vi[1]);
-        load_idx(base + 128, Vi[0]);
         gather_box(v0, Vb[0], Bx[0]);
-        test_and_gather(base, Vb[0], Bx[0], K[0], Dd[0], Dc[0]);   // chunk 0: data in flight
-        gather_box(Vi[1], Vb[1], Bx[1]);                     // chunk 1: box in flight
-        // chunk c's stages use slot c & 1 for data, (c + 1) & 1 for the box and c & 1 for the
-        // index; step c (slot u = c & 1) issues the loads of chunks c+1..c+3, then blends c
-        auto loads = [&](auto U) {
-            constexpr int u = decltype(U)::value, w = u ^ 1;
-            load_idx(base + 192, Vi[w]);                           // chunk c+3
-            gather_box(Vi[u], Vb[u], Bx[u]);                       // chunk c+2
-            test_and_gather(base + 64, Vb[w], Bx[w], K[w], Dd[w], Dc[w]);   // chunk c+1
-            if (STATS) ++st_iter;
-        };
+        // chunk c's stages use slot c & 1 for the box and (c + 1) & 1 for the next index; step c
+        // (slot u = c & 1) issues the loads of chunks c+1..c+2, tests chunk c, then blends the
+        // batch in flight and issues the next one
         auto step = [&](auto U) {
-            constexpr int u = decltype(U)::value;
-            loads(U);
-            // uniform branches; a block that turns sparse mid-chunk leaves the chunk's
-            // remaining survivors in K[u] for the sparse blend
-            if (!sparse && blend_dense(K[u], Dd[u], Dc[u])) go_sparse();
-            if (sparse) blend_sparse(K[u], Dd[u], Dc[u]);
+            constexpr int u = decltype(U)::value, w = u ^ 1;
+            load_idx(base + 128, Vi[u]);       // chunk c+2
+            gather_box(Vi[w], Vb[w], Bx[w]);   // chunk c+1
+            test_and_queue(base, Vb[u], Bx[u]);  // chunk c
+            if (STATS) ++st_iter;
+            if (inflight) blend_batch();
             base += 64;
-            return base < end && !all_done;
+            // past the list's end the steps go on until the queue is drained (their loads re-read
+            // the last entry, their tests take nothing)
+            if (qn >= kBatch || (base >= end && qn)) issue_batch();  // uniform
+            return (base < end || inflight) && !all_done;
         };
         for (;;) {
             if (!step(std::integral_constant<int, 0>{})) break;
