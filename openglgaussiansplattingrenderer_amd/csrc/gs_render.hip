@@ -713,8 +713,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
     __shared__ float s_epow[256 + 64];
     __shared__ uint8_t s_epix[256 + 64];
-    // box survivors queued in list order until a batch is blended (kBatch <= 64; <= 127 queued)
-    __shared__ uint32_t s_q[128];
+    // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
+    __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
     const int L = blockIdx.x;
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
