@@ -1,6 +1,8 @@
 // Issue cost of the vector instructions k_draw's survivor step is made of (tools only):
 // 6 waves per SIMD on every CU, each running 16 independent chains of one instruction type.
 // Prints ns per wave-instruction per SIMD and that in cycles of the v_fma_f32 rate (2 cycles).
+// ds_bpermute (a broadcast through the LDS crossbar) is LDS-throughput bound: ~8.5 v_fma's worth
+// per wave-instruction per SIMD with every SIMD issuing them.
 //   hipcc -O3 --offload-arch=gfx950 -o valu_cost valu_cost.hip && ./valu_cost
 #include <hip/hip_runtime.h>
 
@@ -42,6 +44,11 @@ __global__ __launch_bounds__(64) void k(float *out, float a, float b, unsigned l
                 sacc ^= (unsigned)s;
             }
             if (OP == 9) asm volatile("v_add_f32 %0, %0, %1" : "+v"(acc[i]) : "v"(a));
+            if (OP == 10) {  // ds_bpermute broadcast of lane 5 (LDS crossbar, no LDS storage)
+                unsigned r;
+                asm volatile("ds_bpermute_b32 %0, %1, %2\n s_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(20u), "v"(u[i]));
+                u[i] ^= r;
+            }
         }
     }
     float r = sacc;
@@ -73,12 +80,13 @@ int main() {
     float *out;
     (void)hipMalloc(&out, 4096);
     const char *names[] = {"v_fma_f32", "v_pk_fma_f32", "v_pk_mul_f32", "v_readlane_b32", "v_mbcnt_lo", "v_cndmask(s)",
-                           "v_exp_f32", "v_med3_f32", "v_cmp->sgpr", "v_add_f32"};
+                           "v_exp_f32", "v_med3_f32", "v_cmp->sgpr", "v_add_f32", "ds_bpermute"};
     for (int w : {1, 2, 6}) {
-        float ns[10] = {run<0>(out, w), run<1>(out, w), run<2>(out, w), run<3>(out, w), run<4>(out, w),
-                        run<5>(out, w), run<6>(out, w), run<7>(out, w), run<8>(out, w), run<9>(out, w)};
+        float ns[11] = {run<0>(out, w), run<1>(out, w), run<2>(out, w), run<3>(out, w), run<4>(out, w),
+                        run<5>(out, w), run<6>(out, w), run<7>(out, w), run<8>(out, w), run<9>(out, w),
+                        run<10>(out, w)};
         std::printf("waves/SIMD %d\n", w);
-        for (int i = 0; i < 10; ++i)
+        for (int i = 0; i < 11; ++i)
             std::printf("  %-16s %.3f ns  = %.2f x v_fma (%.2f cyc at the fma's 2)\n", names[i], ns[i], ns[i] / ns[0],
                         2.0f * ns[i] / ns[0]);
     }
