@@ -183,13 +183,21 @@ struct SceneDev {
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
     const float *sh;             // 48 SoA planes (channel c, coefficient k -> plane 16c + k) or null
 };
-// per-splat blend inputs, one 32-byte aligned record (the blend gathers it with the colour)
-struct alignas(32) SplatDraw {
+// per-splat blend inputs, 24 bytes (the blend gathers it with the colour; the pre-exp skip
+// threshold is derived from o where the blend needs it, draw_threshold)
+struct alignas(8) SplatDraw {
     float mx, my;      // screen position (preprocess.glsl:91-94)
     float a, b, c, o;  // conic (:134-136) and opacity
-    float thr;         // pre-exp skip threshold -ln(255 o) - 1e-3
-    float pad;
 };
+static_assert(sizeof(SplatDraw) == 24, "24-byte blend records");
+// the blend's pre-exp skip threshold: power < thr implies alpha < 1/255 (draw.glsl:123-126) for
+// any exp within a few ulp; 255 o <= 0 gives +inf (never blends), NaN (opacity NaN) -inf (never
+// skips).  v_log_f32 (margins far above its error); the box of the preprocess uses the same log.
+__device__ __forceinline__ float draw_log255o(float o) { return __logf(255.0f * o); }
+__device__ __forceinline__ float draw_threshold(float o) {
+    const float thr = -draw_log255o(o) - 1.0e-3f;
+    return thr != thr ? -__builtin_inff() : thr;
+}
 struct FrameDev {
     SplatDraw *sd;
     uint2 *cullbox;    // conservative pixel box of the alpha >= 1/255 region (int16 bounds, pack_box)

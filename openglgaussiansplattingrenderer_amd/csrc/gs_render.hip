@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
         // v_sqrt instead of the correctly rounded library sequences.
         const float A = cov2.x, B = cov2.y, Cq = cov2.z;
-        const float lg = __logf(255.0f * opac);  // ln(255 o)
+        const float lg = draw_log255o(opac);  // ln(255 o)
         const float tau = lg + 0.05f;
         const float detQ = A * Cq - B * B;
         const float trq = A + Cq;
@@ -292,9 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         // reached by a Q10 over-read; k_draw): without entries its record is the culled one --
         // means2D, conic and opacity 0 (never blends: threshold +inf, empty box)
         if (rc.y >= 0) {
-        float thr = -lg - 1.0e-3f;
-        if (thr != thr) thr = -__builtin_inff();
-        fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w, thr, 0.0f};
+        fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w};
         fr.cullbox[i] = pack_box(box);
         if (P.sh) {  // GS_FLAG_SH: this frame's colour
             float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
@@ -308,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         }
         }
         else if (i == 0) {  // splat 0 culled: the record its culled entries draw
-            fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, __builtin_inff(), 0.0f};
+            fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // threshold +inf
             fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
         }
         if (PACK)
@@ -691,10 +689,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct alignas(16) SurvData {
     float mx, my, a, b, c, o, thr;
 };
+struct alignas(8) SurvLoad {  // SplatDraw as gathered (dwordx4 + dwordx2)
+    float mx, my, a, b, c, o;
+};
 struct alignas(16) SurvRgb {
     float x, y, z;
 };
-static_assert(offsetof(SplatDraw, thr) == offsetof(SurvData, thr), "SurvData mirrors SplatDraw");
+static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw");
 
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
@@ -916,7 +917,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         const uint32_t bn = min(qn, 64u);
         const uint32_t id = s_q[min((uint32_t)lane, bn - 1u)];
         // the 7 used floats of the SplatDraw record and rgb of the colour
-        Dd = *at(reinterpret_cast<const SurvData *>(sd), id << 5);
+        const SurvLoad ld = *at(reinterpret_cast<const SurvLoad *>(sd), id * (uint32_t)sizeof(SplatDraw));
+        Dd = SurvData{ld.mx, ld.my, ld.a, ld.b, ld.c, ld.o, 0.0f};  // thr: once the data arrived (blend_batch)
         Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
         bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
         if (qn > 64u) {  // uniform, rare
@@ -1090,6 +1092,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
 
     // the batch in flight: exact cull and blend (its data arrived; uniform branches)
     auto blend_batch = [&]() __attribute__((always_inline)) {
+        Dd.thr = draw_threshold(Dd.o);
         if (!sparse && blend_dense(bk, Dd, Dc)) go_sparse();
         if (sparse) blend_sparse(bk, Dd, Dc);
         inflight = false;
