@@ -256,11 +256,12 @@ int gs_timing_enable(gs_ctx *ctx, int mode);
  * block duration in s_memrealtime ticks (100 MHz), [8] (wave, survivor) steps, [9] steps where some pixel
  * of the wave needs the exp/blend path, [10] (pixel, survivor) pairs needing it */
 int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset);
-/* per-block trace of the last GS_FLAG_DRAW_STATS draw, 12 uint32 per block in launch order:
+/* per-block trace of the last GS_FLAG_DRAW_STATS draw, 16 uint32 per block in launch order:
  * start, end (s_memrealtime ticks, 100 MHz, low 32 bits), iterations, survivors, (wave,
  * survivor) steps, steps with a needing pixel, (pixel, survivor) needs, list entries in range,
  * survivor steps while <= 64 / <= 128 pixels of the block were active, events while <= 64
- * were, ticks from the block's start until <= 64 were (0: never).
+ * were, ticks from the block's start until <= 64 were (0: never), dense-phase survivor steps
+ * with > 192 / 129-192 / 65-128 active pixels, dense-phase blend events.
  * Returns the number of blocks copied (<= max_blocks, <= 65536). */
 int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks);
 int gs_timing_read(gs_ctx *ctx, gs_timing *out);

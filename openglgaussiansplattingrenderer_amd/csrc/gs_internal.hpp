@@ -227,10 +227,11 @@ void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, i
 // GS_FLAG_DRAW_STATS buffer: per block (launch order) kDrawTraceWords uint32: start, end
 // (s_memrealtime, 100 MHz), steps, survivors, (wave, survivor) steps, steps with a needing
 // pixel, (pixel, survivor) needs, list entries in range, survivor steps while <= 64 / <= 128
-// pixels were active, events while <= 64 were, ticks until <= 64 were; the host aggregates
+// pixels were active, events while <= 64 were, ticks until <= 64 were, dense-phase survivor
+// steps with > 192 / 129-192 / 65-128 active pixels, dense-phase events; the host aggregates
 // (gs_draw_stats)
 constexpr int kDrawTraceBlocks = 65536;
-constexpr int kDrawTraceWords = 12;
+constexpr int kDrawTraceWords = 16;
 constexpr size_t kDrawStatsBytes = (size_t)kDrawTraceBlocks * kDrawTraceWords * 4;
 
 void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,

@@ -700,8 +700,18 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
+#ifndef GS_DRAW_LOOP2
+#define GS_DRAW_LOOP2 1
+#endif
+// blend events compacted with exec-masked LDS writes (no spare entries): 5760 B of LDS per wave
+#ifndef GS_DRAW_MASKED_EV
+#define GS_DRAW_MASKED_EV 1
+#endif
+#ifndef GS_DRAW_WAVES
+#define GS_DRAW_WAVES (GS_DRAW_MASKED_EV ? 7 : 6)
+#endif
 template <bool FAST_EXP, bool STATS>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVES))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
                                              const uint2 *__restrict__ cullbox,
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
@@ -712,8 +722,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     __shared__ float4 s_col[256];
     // one survivor's blend events: power and pixel id (split), entries 256 + lane take the
     // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
-    __shared__ float s_epow[256 + 64];
-    __shared__ uint8_t s_epix[256 + 64];
+    constexpr int kSpare = GS_DRAW_MASKED_EV ? 0 : 64;
+    __shared__ float s_epow[256 + kSpare];
+    __shared__ uint8_t s_epix[256 + kSpare];
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
@@ -786,6 +797,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_t64 = 0;
+    unsigned long long st_a192 = 0, st_a128 = 0, st_a64 = 0, st_dev = 0;  // dense steps by active pixels
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
     const int jmax = max(end - 1, 0);
@@ -828,11 +840,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         const uint64_t A0 = ~D0, A1 = ~D1, A2 = ~D2, A3 = ~D3;
         const uint32_t a0 = (uint32_t)__popcll(A0), a1 = (uint32_t)__popcll(A1), a2 = (uint32_t)__popcll(A2);
         nact = a0 + a1 + a2 + (uint32_t)__popcll(A3);
+#if GS_DRAW_MASKED_EV
+        if (__builtin_amdgcn_inverse_ballot_w64(A0)) s_epix[below(A0, 0)] = (uint8_t)(4 * lane + 0);
+        if (__builtin_amdgcn_inverse_ballot_w64(A1)) s_epix[below(A1, a0)] = (uint8_t)(4 * lane + 1);
+        if (__builtin_amdgcn_inverse_ballot_w64(A2)) s_epix[below(A2, a0 + a1)] = (uint8_t)(4 * lane + 2);
+        if (__builtin_amdgcn_inverse_ballot_w64(A3)) s_epix[below(A3, a0 + a1 + a2)] = (uint8_t)(4 * lane + 3);
+#else
         const uint32_t spare = 256u + (uint32_t)lane;
         s_epix[((A0 >> lane) & 1) ? below(A0, 0) : spare] = (uint8_t)(4 * lane + 0);
         s_epix[((A1 >> lane) & 1) ? below(A1, a0) : spare] = (uint8_t)(4 * lane + 1);
         s_epix[((A2 >> lane) & 1) ? below(A2, a0 + a1) : spare] = (uint8_t)(4 * lane + 2);
         s_epix[((A3 >> lane) & 1) ? below(A3, a0 + a1 + a2) : spare] = (uint8_t)(4 * lane + 3);
+#endif
         wave_lds_sync();
         spix = s_epix[min((uint32_t)lane, nact - 1)];
         SA = nact >= 64 ? ~0ull : ((1ull << nact) - 1);
@@ -942,9 +961,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         // one exit (a uniform loop condition, no continue / return inside): fewer scalar
         // control-flow instructions per survivor
         bool turned = false, stop = all_done;  // stop = all_done | turned, set only on a refresh
+#if GS_DRAW_LOOP2
+        // single-exit loop on the survivors left (km): a few scalar instructions of loop control
+        // per survivor; a refresh that stops the block hands the rest back in keep and ends it
+        uint64_t km = all_done ? 0ull : keep;
+        keep = 0;
+        if (km) do {
+            const int src = __builtin_ctzll(km);
+            km &= ~(1ull << src);
+#else
         while (keep && !stop) {
             const int src = __builtin_ctzll(keep);
             keep &= keep - 1;
+#endif
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
             const float thr = rl(d.thr, src);
@@ -976,11 +1005,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 if (active <= 64 && st_t64 == 0) st_t64 = __builtin_amdgcn_s_memrealtime() - st_t0;
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
+                st_a192 += active > 192 ? 1 : 0;
+                st_a128 += (active > 128 && active <= 192) ? 1 : 0;
+                st_a64 += (active > 64 && active <= 128) ? 1 : 0;
+                st_dev += nev;
             }
             if (nev != 0) {  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
             // v_mbcnt); each pixel occurs at most once, so the events are independent.  Every
             // lane writes each slot: lanes without that event into their own spare entry.
+#if GS_DRAW_MASKED_EV
+            // (exec-masked writes: the uniform masks are the branch conditions as they are)
+            if (__builtin_amdgcn_inverse_ballot_w64(b0)) {
+                const uint32_t e = below(b0, 0);
+                s_epow[e] = p00;
+                s_epix[e] = (uint8_t)(4 * lane + 0);
+            }
+            if (__builtin_amdgcn_inverse_ballot_w64(b1)) {
+                const uint32_t e = below(b1, e0);
+                s_epow[e] = p10;
+                s_epix[e] = (uint8_t)(4 * lane + 1);
+            }
+            if (__builtin_amdgcn_inverse_ballot_w64(b2)) {
+                const uint32_t e = below(b2, e0 + e1);
+                s_epow[e] = p01;
+                s_epix[e] = (uint8_t)(4 * lane + 2);
+            }
+            if (__builtin_amdgcn_inverse_ballot_w64(b3)) {
+                const uint32_t e = below(b3, e0 + e1 + e2);
+                s_epow[e] = p11;
+                s_epix[e] = (uint8_t)(4 * lane + 3);
+            }
+#else
             const uint32_t spare = 256u + (uint32_t)lane;
             {
                 const uint32_t e = sel_u32(spare, below(b0, 0), b0);
@@ -1002,6 +1058,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 s_epow[e] = p11;
                 s_epix[e] = (uint8_t)(4 * lane + 3);
             }
+#endif
             wave_lds_sync();
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
@@ -1039,10 +1096,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
                 turned = !all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64;
                 stop = all_done | turned;
+#if GS_DRAW_LOOP2
+                if (stop) {
+                    keep = km;
+                    km = 0;
+                }
+#endif
             }
             wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
             }
+#if GS_DRAW_LOOP2
+        } while (km);
+#else
         }
+#endif
         return turned;
     };
 
@@ -1054,9 +1121,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
         if (!keep) return;  // uniform
         const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
         const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
+#if GS_DRAW_LOOP2
+        uint64_t km = all_done ? 0ull : keep;  // single-exit loop, as in blend_dense
+        if (km) do {
+            const int src = __builtin_ctzll(km);
+            km &= ~(1ull << src);
+#else
         while (keep && !all_done) {
             const int src = __builtin_ctzll(keep);
             keep &= keep - 1;
+#endif
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
             const float thr = rl(d.thr, src);
@@ -1086,8 +1160,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
                 pc.w = take ? pc.w + aT : pc.w;
                 SA &= ~ballot(pc.w >= 0.99f);  // :129-133
                 all_done = SA == 0;
+#if GS_DRAW_LOOP2
+                if (all_done) km = 0;
+#endif
             }
+#if GS_DRAW_LOOP2
+        } while (km);
+#else
         }
+#endif
     };
 
     // the batch in flight: exact cull and blend (its data arrived; uniform branches)
@@ -1155,6 +1236,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void k_
             tr[9] = (uint32_t)st_kit128;
             tr[10] = (uint32_t)st_ev64;
             tr[11] = (uint32_t)st_t64;
+            tr[12] = (uint32_t)st_a192;
+            tr[13] = (uint32_t)st_a128;
+            tr[14] = (uint32_t)st_a64;
+            tr[15] = (uint32_t)st_dev;
         }
     }
 }

@@ -90,8 +90,9 @@ class Context:
     def draw_block_trace(self, blocks: int) -> np.ndarray:
         """[blocks, 12] uint32 per draw block (gs_draw_block_trace): start, end (100 MHz ticks),
         iterations, survivors, survivor steps, steps with a needing pixel, pixel needs, list
-        entries, steps while <= 64 / <= 128 pixels active, events while <= 64, ticks to <= 64."""
-        a = np.zeros((blocks, 12), np.uint32)
+        entries, steps while <= 64 / <= 128 pixels active, events while <= 64, ticks to <= 64,
+        dense-phase steps with > 192 / 129-192 / 65-128 active pixels, dense-phase events."""
+        a = np.zeros((blocks, 16), np.uint32)
         n = lib().gs_draw_block_trace(self.handle, ptr(a), int(blocks))
         check(n, self.handle)
         return a[:n]

@@ -64,4 +64,8 @@ print(f"survivor steps {tr[:, 4].sum()}: with <=64 active px {k64} ({k64 / tr[:,
 r = t64[t64 > 0] * 0.01
 print(f"blocks reaching <=64 active: {len(r)}; time to reach it / duration: "
       f"{np.median(t64[t64 > 0] * 0.01 / d[t64 > 0]):.2f} (median)")
+a192, a128, a64, dev = (tr[:, k].sum() for k in (12, 13, 14, 15))
+nd = a192 + a128 + a64
+print(f"dense steps {nd}: >192 active {a192} ({a192 / nd:.1%}), 129-192 {a128} ({a128 / nd:.1%}), "
+      f"65-128 {a64} ({a64 / nd:.1%}); events per dense step {dev / nd:.1f}")
 print("counters:", st)
