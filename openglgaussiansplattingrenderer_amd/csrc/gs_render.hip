@@ -77,8 +77,9 @@ __device__ __forceinline__ float exp_defined_event(float x) {
     t = __builtin_fmaf(t, r, 0.5f);
     t = __builtin_fmaf(t, r, 1.0f);
     const float p = __builtin_fmaf(t, r, 1.0f);
-    const int k = (int)kf;
-    const float v = p * u2f((uint32_t)(k + 127) << 23);
+    // p * 2^k: for x in [-80, 0] k is in [-116, 0] and p in [0.7, 1.42], so 2^k and the product
+    // are normal and exact: v_ldexp_f32 gives the oracle's p * u2f((k + 127) << 23) in one op
+    const float v = __builtin_amdgcn_ldexpf(p, (int)kf);
     return (x >= -80.0f) ? v : 0.0f;
 }
 
@@ -898,6 +899,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     SurvData Dd;                // the batch's survivor data (lane j: survivor j)
     SurvRgb Dc;                 // ... colour
     uint64_t bk = 0;            // the batch's lanes (uniform)
+    bool cfin = true;           // every colour of the batch is finite (uniform)
     uint32_t qn = 0;            // survivors queued (uniform)
     bool inflight = false;      // a batch's data gather is in flight (uniform)
 
@@ -1074,10 +1076,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 // alphaBlend :59-67
                 const float remaining = 1.0f - col.w;
                 const float aT = alpha * remaining;
-                col.x = take ? col.x + r * aT : col.x;
-                col.y = take ? col.y + g * aT : col.y;
-                col.z = take ? col.z + bl * aT : col.z;
-                col.w = take ? col.w + aT : col.w;
+                if (cfin) {  // uniform: finite colours -- adding rgb * 0 leaves the state as it is
+                    const float aZ = take ? aT : 0.0f;
+                    col.x = col.x + r * aZ;
+                    col.y = col.y + g * aZ;
+                    col.z = col.z + bl * aZ;
+                    col.w = col.w + aZ;
+                } else {
+                    col.x = take ? col.x + r * aT : col.x;
+                    col.y = take ? col.y + g * aT : col.y;
+                    col.z = take ? col.z + bl * aT : col.z;
+                    col.w = take ? col.w + aT : col.w;
+                }
                 s_col[pix] = col;
                 sat = max(sat, __float_as_uint(col.w));  // :129-133
             };
@@ -1151,13 +1161,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
                 const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
                 const float alpha = fminf(0.99f, ex * o);
-                const bool take = ((nb >> lane) & 1) & !(alpha < 1.0f / 255.0f);
+                const bool take = __builtin_amdgcn_inverse_ballot_w64(nb) & !(alpha < 1.0f / 255.0f);
                 // alphaBlend :59-67
                 const float aT = alpha * (1.0f - pc.w);
-                pc.x = take ? pc.x + r * aT : pc.x;
-                pc.y = take ? pc.y + g * aT : pc.y;
-                pc.z = take ? pc.z + bl * aT : pc.z;
-                pc.w = take ? pc.w + aT : pc.w;
+                if (cfin) {  // uniform (see the dense event)
+                    const float aZ = take ? aT : 0.0f;
+                    pc.x = pc.x + r * aZ;
+                    pc.y = pc.y + g * aZ;
+                    pc.z = pc.z + bl * aZ;
+                    pc.w = pc.w + aZ;
+                } else {
+                    pc.x = take ? pc.x + r * aT : pc.x;
+                    pc.y = take ? pc.y + g * aT : pc.y;
+                    pc.z = take ? pc.z + bl * aT : pc.z;
+                    pc.w = take ? pc.w + aT : pc.w;
+                }
                 SA &= ~ballot(pc.w >= 0.99f);  // :129-133
                 all_done = SA == 0;
 #if GS_DRAW_LOOP2
@@ -1174,6 +1192,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // the batch in flight: exact cull and blend (its data arrived; uniform branches)
     auto blend_batch = [&]() __attribute__((always_inline)) {
         Dd.thr = draw_threshold(Dd.o);
+        // A blend that does not take an event adds rgb * 0 (and 0 to w) instead of keeping the
+        // state by selects: the same bits when every colour of the batch is finite (the state's
+        // channels are never -0, and x + (+-0) == x otherwise); a non-finite colour (inf * 0 is
+        // NaN) keeps the selects.
+        cfin = ballot(!(__builtin_isfinite(Dc.x) & __builtin_isfinite(Dc.y) & __builtin_isfinite(Dc.z))) == 0;
         if (!sparse && blend_dense(bk, Dd, Dc)) go_sparse();
         if (sparse) blend_sparse(bk, Dd, Dc);
         inflight = false;
