@@ -24,16 +24,26 @@ namespace {
 
 constexpr int kBlock = 256;
 
+#ifndef GS_F2I_CVT
+#define GS_F2I_CVT 1
+#endif
 __device__ __forceinline__ uint32_t f2u(float f) { return __float_as_uint(f); }
 __device__ __forceinline__ float u2f(uint32_t u) { return __uint_as_float(u); }
 
-// GLSL int(float) with v_cvt_i32_f32's out-of-range behaviour (saturate, NaN -> 0),
-// written out so the compiler cannot exploit C++'s UB on out-of-range conversions.
+// GLSL int(float) with v_cvt_i32_f32's out-of-range behaviour (saturate, NaN -> 0): the
+// instruction itself (C++'s conversion is UB out of range, and the explicit checks compiled to
+// three nested exec-mask branches per conversion; tools/micro/cvt_check.hip pins the two equal)
 __device__ __forceinline__ int f2i(float f) {
+#if GS_F2I_CVT
+    int r;
+    asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+    return r;
+#else
     if (f != f) return 0;
     if (f >= 2147483648.0f) return 2147483647;
     if (f <= -2147483648.0f) return (-2147483647 - 1);
     return (int)f;
+#endif
 }
 
 // glm operator*(mat4, vec4): (m0*x + m1*y) + (m2*z + m3*w)
