@@ -184,7 +184,9 @@ __device__ __forceinline__ uint2 pack_box(const float4 &b) {
     return make_uint2(lo(b.x) | (hi(b.y) << 16), lo(b.z) | (hi(b.w) << 16));
 }
 
-template <bool PACK>
+// CLEAN: clean mode (P.clean) as a template parameter -- a uniform flag's alternatives were
+// if-converted into selects that every splat evaluated
+template <bool PACK, bool CLEAN>
 __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_wave[kBlock / 64];
     uint32_t n_main = 0, n_dup = 0;
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         const float sz = (p2 + 1.0f) * 0.5f;
         sx = sx * (float)P.W;
         sy = sy * (float)P.H;
-        if (P.clean) vis = vis && (sz >= 0.0f && sz <= 1.0f);  // clean: near/far cull (Q6)
+        if (CLEAN) vis = vis && (sz >= 0.0f && sz <= 1.0f);  // clean: near/far cull (Q6)
         // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
         const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
         const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
@@ -244,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
         const float det = ca * cc - cb * cb;
         vis = vis && det != 0;  // Q7: entry omitted
-        if (P.clean) vis = vis && det > 0.0f;
+        if (CLEAN) vis = vis && det > 0.0f;
         const float inv = 1.0f / det;
         const float4 cov2 = make_float4(cc * inv, -cb * inv, ca * inv, opac);
         // :139-149
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         const int maxY = min(15, f2i((sy + radius) / P.tile_h));
         // :151-155 main tile (unclamped in ref mode, Q5)
         int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
-        if (P.clean) {
+        if (CLEAN) {
             tileX = min(15, max(0, tileX));
             tileY = min(15, max(0, tileY));
         }
@@ -1288,8 +1290,12 @@ bool rec_packed(const PreParams &P) { return P.clean || (P.W >= 16 && P.H >= 16)
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start) {
     const int nb = preprocess_blocks(P.n);
     if (nb <= 0) return;
-    if (rec_packed(P)) hipExtLaunchKernelGGL(k_preprocess<true>, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
-    else hipExtLaunchKernelGGL(k_preprocess<false>, dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+    if (P.clean)  // (clean mode always packs its records)
+        hipExtLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+    else if (rec_packed(P))
+        hipExtLaunchKernelGGL((k_preprocess<true, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+    else
+        hipExtLaunchKernelGGL((k_preprocess<false, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
