@@ -74,8 +74,19 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # timing / barrier plumbing only: gloo on the host (there is no data-path collective)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # timing / barrier plumbing only: gloo on the host (there is no data-path collective).
+        # Gloo prints its connection lines on fd 1; they go to stderr so that stdout holds the
+        # JSON line alone.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         pg = dist
     return world, rank, local, pg
 

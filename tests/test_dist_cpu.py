@@ -69,12 +69,31 @@ def test_gpus_flag_spawns_ranks():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--dry-run"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout  # the JSON line alone (gloo's connection lines go to stderr)
     d = json.loads(lines[0])
     assert d["dry_run"] and d["n_gpus"] == 3 and d["max_over_ranks"] == 3.0
     assert [x["rank"] for x in d["ranks"]] == [0, 1, 2] and [x["view"] for x in d["ranks"]] == [0, 1, 2]
     assert len({tuple(x["view_matrix"]) for x in d["ranks"]}) == 3  # each rank its own pose
+
+
+def test_torchrun_launch_prints_one_line():
+    """the driver's N > 1 launch: `torch.distributed.run --nproc-per-node N bench.py --gpus N`
+    (dry run); stdout is rank 0's JSON line and nothing else"""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and [x["view"] for x in d["ranks"]] == [0, 1]
 
 
 def test_failing_rank_ends_the_spawn():
