@@ -726,9 +726,6 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
-#ifndef GS_DRAW_LOOP2
-#define GS_DRAW_LOOP2 1
-#endif
 // blend events compacted with exec-masked LDS writes (no spare entries): 5760 B of LDS per wave
 #ifndef GS_DRAW_MASKED_EV
 #define GS_DRAW_MASKED_EV 1
@@ -743,8 +740,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                                              const SplatDraw *__restrict__ sd, const float4 *__restrict__ colour,
                                              uint32_t *__restrict__ out, unsigned long long *__restrict__ stats,
                                              uint32_t *fr_h_totals) {
-    // pixel state, pixel id = 4*lane + slot; a pixel is done (:129-133) iff its w >= 0.99 (pixels
-    // outside the image start at w = 1)
+    // pixel state, pixel id = 16*y + x in the sub-block; a pixel is done (:129-133) iff its
+    // w >= 0.99 (pixels outside the image start at w = 1)
     __shared__ float4 s_col[256];
     // one survivor's blend events: power and pixel id (split), entries 256 + lane take the
     // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
@@ -816,10 +813,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int qmax = max(E - 1, 0);
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
+    // pixel ids are row-major in the sub-block (16 * y + x): the lane's quad is qbase + kQuad[k]
+    const uint32_t qbase = 32u * ((uint32_t)lane >> 3) + 2u * ((uint32_t)lane & 7u);
+    constexpr uint32_t kQuad[4] = {0u, 1u, 16u, 17u};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const bool dk = k == 0 ? d00 : k == 1 ? d10 : k == 2 ? d01 : d11;
-        s_col[4 * lane + k] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
+        s_col[qbase + kQuad[k]] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_t64 = 0;
@@ -867,22 +867,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         const uint32_t a0 = (uint32_t)__popcll(A0), a1 = (uint32_t)__popcll(A1), a2 = (uint32_t)__popcll(A2);
         nact = a0 + a1 + a2 + (uint32_t)__popcll(A3);
 #if GS_DRAW_MASKED_EV
-        if (__builtin_amdgcn_inverse_ballot_w64(A0)) s_epix[below(A0, 0)] = (uint8_t)(4 * lane + 0);
-        if (__builtin_amdgcn_inverse_ballot_w64(A1)) s_epix[below(A1, a0)] = (uint8_t)(4 * lane + 1);
-        if (__builtin_amdgcn_inverse_ballot_w64(A2)) s_epix[below(A2, a0 + a1)] = (uint8_t)(4 * lane + 2);
-        if (__builtin_amdgcn_inverse_ballot_w64(A3)) s_epix[below(A3, a0 + a1 + a2)] = (uint8_t)(4 * lane + 3);
+        if (__builtin_amdgcn_inverse_ballot_w64(A0)) s_epix[below(A0, 0)] = (uint8_t)(qbase + kQuad[0]);
+        if (__builtin_amdgcn_inverse_ballot_w64(A1)) s_epix[below(A1, a0)] = (uint8_t)(qbase + kQuad[1]);
+        if (__builtin_amdgcn_inverse_ballot_w64(A2)) s_epix[below(A2, a0 + a1)] = (uint8_t)(qbase + kQuad[2]);
+        if (__builtin_amdgcn_inverse_ballot_w64(A3)) s_epix[below(A3, a0 + a1 + a2)] = (uint8_t)(qbase + kQuad[3]);
 #else
         const uint32_t spare = 256u + (uint32_t)lane;
-        s_epix[((A0 >> lane) & 1) ? below(A0, 0) : spare] = (uint8_t)(4 * lane + 0);
-        s_epix[((A1 >> lane) & 1) ? below(A1, a0) : spare] = (uint8_t)(4 * lane + 1);
-        s_epix[((A2 >> lane) & 1) ? below(A2, a0 + a1) : spare] = (uint8_t)(4 * lane + 2);
-        s_epix[((A3 >> lane) & 1) ? below(A3, a0 + a1 + a2) : spare] = (uint8_t)(4 * lane + 3);
+        s_epix[((A0 >> lane) & 1) ? below(A0, 0) : spare] = (uint8_t)(qbase + kQuad[0]);
+        s_epix[((A1 >> lane) & 1) ? below(A1, a0) : spare] = (uint8_t)(qbase + kQuad[1]);
+        s_epix[((A2 >> lane) & 1) ? below(A2, a0 + a1) : spare] = (uint8_t)(qbase + kQuad[2]);
+        s_epix[((A3 >> lane) & 1) ? below(A3, a0 + a1 + a2) : spare] = (uint8_t)(qbase + kQuad[3]);
 #endif
         wave_lds_sync();
         spix = s_epix[min((uint32_t)lane, nact - 1)];
         SA = nact >= 64 ? ~0ull : ((1ull << nact) - 1);
-        const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
-        const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
+        const float sfx = (float)(x0 + (int)(spix & 15u));
+        const float sfy = (float)(y0 + (int)(spix >> 4));
         float mnx = sfx, mxx = sfx, mny = sfy, mxy = sfy;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -988,19 +988,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // one exit (a uniform loop condition, no continue / return inside): fewer scalar
         // control-flow instructions per survivor
         bool turned = false, stop = all_done;  // stop = all_done | turned, set only on a refresh
-#if GS_DRAW_LOOP2
         // single-exit loop on the survivors left (km): a few scalar instructions of loop control
         // per survivor; a refresh that stops the block hands the rest back in keep and ends it
         uint64_t km = all_done ? 0ull : keep;
         keep = 0;
+        // a survivor saturated a pixel (rare): the done masks again from the pixel state; a stop
+        // hands the survivors left back in keep and ends the loop
+        auto refresh = [&]() {
+            wave_lds_sync();
+            D0 = ballot(s_col[qbase + kQuad[0]].w >= 0.99f);
+            D1 = ballot(s_col[qbase + kQuad[1]].w >= 0.99f);
+            D2 = ballot(s_col[qbase + kQuad[2]].w >= 0.99f);
+            D3 = ballot(s_col[qbase + kQuad[3]].w >= 0.99f);
+            all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
+            turned = !all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64;
+            stop = all_done | turned;
+            if (stop) {
+                keep = km;
+                km = 0;
+            }
+        };
         if (km) do {
             const int src = __builtin_ctzll(km);
             km &= ~(1ull << src);
-#else
-        while (keep && !stop) {
-            const int src = __builtin_ctzll(keep);
-            keep &= keep - 1;
-#endif
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
             const float thr = rl(d.thr, src);
@@ -1046,44 +1056,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             if (__builtin_amdgcn_inverse_ballot_w64(b0)) {
                 const uint32_t e = below(b0, 0);
                 s_epow[e] = p00;
-                s_epix[e] = (uint8_t)(4 * lane + 0);
+                s_epix[e] = (uint8_t)(qbase + kQuad[0]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b1)) {
                 const uint32_t e = below(b1, e0);
                 s_epow[e] = p10;
-                s_epix[e] = (uint8_t)(4 * lane + 1);
+                s_epix[e] = (uint8_t)(qbase + kQuad[1]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b2)) {
                 const uint32_t e = below(b2, e0 + e1);
                 s_epow[e] = p01;
-                s_epix[e] = (uint8_t)(4 * lane + 2);
+                s_epix[e] = (uint8_t)(qbase + kQuad[2]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b3)) {
                 const uint32_t e = below(b3, e0 + e1 + e2);
                 s_epow[e] = p11;
-                s_epix[e] = (uint8_t)(4 * lane + 3);
+                s_epix[e] = (uint8_t)(qbase + kQuad[3]);
             }
 #else
             const uint32_t spare = 256u + (uint32_t)lane;
             {
                 const uint32_t e = sel_u32(spare, below(b0, 0), b0);
                 s_epow[e] = p00;
-                s_epix[e] = (uint8_t)(4 * lane + 0);
+                s_epix[e] = (uint8_t)(qbase + kQuad[0]);
             }
             {
                 const uint32_t e = sel_u32(spare, below(b1, e0), b1);
                 s_epow[e] = p10;
-                s_epix[e] = (uint8_t)(4 * lane + 1);
+                s_epix[e] = (uint8_t)(qbase + kQuad[1]);
             }
             {
                 const uint32_t e = sel_u32(spare, below(b2, e0 + e1), b2);
                 s_epow[e] = p01;
-                s_epix[e] = (uint8_t)(4 * lane + 2);
+                s_epix[e] = (uint8_t)(qbase + kQuad[2]);
             }
             {
                 const uint32_t e = sel_u32(spare, below(b3, e0 + e1 + e2), b3);
                 s_epow[e] = p11;
-                s_epix[e] = (uint8_t)(4 * lane + 3);
+                s_epix[e] = (uint8_t)(qbase + kQuad[3]);
             }
 #endif
             wave_lds_sync();
@@ -1122,29 +1132,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             // rare: more events than lanes -- uniform passes, lanes past the end repeat the
             // pass's last event (which no earlier pass held)
             for (uint32_t e0p = 64; e0p < nev; e0p += 64) event(min(e0p + (uint32_t)lane, nev - 1u));
-            if (ballot(sat >= __float_as_uint(0.99f))) {  // uniform, rare: a pixel saturated -- refresh the done masks
-                wave_lds_sync();
-                D0 = ballot(s_col[4 * lane + 0].w >= 0.99f);
-                D1 = ballot(s_col[4 * lane + 1].w >= 0.99f);
-                D2 = ballot(s_col[4 * lane + 2].w >= 0.99f);
-                D3 = ballot(s_col[4 * lane + 3].w >= 0.99f);
-                all_done = (D0 & D1 & D2 & D3) == ~0ull;  // every pixel saturated
-                turned = !all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64;
-                stop = all_done | turned;
-#if GS_DRAW_LOOP2
-                if (stop) {
-                    keep = km;
-                    km = 0;
-                }
-#endif
-            }
+            if (ballot(sat >= __float_as_uint(0.99f))) refresh();  // uniform, rare: a pixel saturated
             wave_lds_sync();  // the next survivor's compaction overwrites s_epow / s_epix
             }
-#if GS_DRAW_LOOP2
         } while (km);
-#else
-        }
-#endif
         return turned;
     };
 
@@ -1154,18 +1145,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         if (!keep) return;  // uniform
-        const float sfx = (float)(x0 + 2 * ((spix >> 2) & 7) + (spix & 1));
-        const float sfy = (float)(y0 + 2 * (spix >> 5) + ((spix >> 1) & 1));
-#if GS_DRAW_LOOP2
+        const float sfx = (float)(x0 + (int)(spix & 15u));
+        const float sfy = (float)(y0 + (int)(spix >> 4));
         uint64_t km = all_done ? 0ull : keep;  // single-exit loop, as in blend_dense
         if (km) do {
             const int src = __builtin_ctzll(km);
             km &= ~(1ull << src);
-#else
-        while (keep && !all_done) {
-            const int src = __builtin_ctzll(keep);
-            keep &= keep - 1;
-#endif
             const float mx = rl(d.mx, src), my = rl(d.my, src);
             const float ca = rl(d.a, src), cbv = rl(d.b, src), cc = rl(d.c, src);
             const float thr = rl(d.thr, src);
@@ -1203,15 +1188,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 }
                 SA &= ~ballot(pc.w >= 0.99f);  // :129-133
                 all_done = SA == 0;
-#if GS_DRAW_LOOP2
                 if (all_done) km = 0;
-#endif
             }
-#if GS_DRAW_LOOP2
         } while (km);
-#else
-        }
-#endif
     };
 
     // the batch in flight: exact cull and blend (its data arrived; uniform branches)
@@ -1262,11 +1241,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
        // spilled there, a private segment in the dominant kernel)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + 2 * (l2 & 7), qy = y0 + 2 * (l2 >> 3);
+        const int qb = 32 * (l2 >> 3) + 2 * (l2 & 7);
         uint32_t *row0 = out + (size_t)qy * P.W + qx, *row1 = row0 + P.W;
-        if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[4 * l2 + 0]);
-        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[4 * l2 + 1]);
-        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[4 * l2 + 2]);
-        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[4 * l2 + 3]);
+        if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
+        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + 1]);
+        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + 16]);
+        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + 17]);
     }
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
