@@ -227,7 +227,7 @@ void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, i
 // GS_FLAG_DRAW_STATS buffer: per block (launch order) kDrawTraceWords uint32: start, end
 // (s_memrealtime, 100 MHz), steps, survivors, (wave, survivor) steps, steps with a needing
 // pixel, (pixel, survivor) needs, list entries in range, survivor steps while <= 64 / <= 128
-// pixels were active, events while <= 64 were, ticks until <= 64 were, dense-phase survivor
+// pixels were active, events while <= 64 were, done-mask refreshes, dense-phase survivor
 // steps with > 192 / 129-192 / 65-128 active pixels, dense-phase events; the host aggregates
 // (gs_draw_stats)
 constexpr int kDrawTraceBlocks = 65536;

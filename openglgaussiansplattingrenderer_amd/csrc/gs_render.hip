@@ -822,7 +822,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         s_col[qbase + kQuad[k]] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
-    unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_t64 = 0;
+    unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_refresh = 0;
     unsigned long long st_a192 = 0, st_a128 = 0, st_a64 = 0, st_dev = 0;  // dense steps by active pixels
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
@@ -995,6 +995,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // a survivor saturated a pixel (rare): the done masks again from the pixel state; a stop
         // hands the survivors left back in keep and ends the loop
         auto refresh = [&]() {
+            if (STATS) ++st_refresh;
             wave_lds_sync();
             D0 = ballot(s_col[qbase + kQuad[0]].w >= 0.99f);
             D1 = ballot(s_col[qbase + kQuad[1]].w >= 0.99f);
@@ -1039,7 +1040,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 st_kit64 += active <= 64 ? 1 : 0;
                 st_kit128 += active <= 128 ? 1 : 0;
                 st_ev64 += active <= 64 ? nev : 0;
-                if (active <= 64 && st_t64 == 0) st_t64 = __builtin_amdgcn_s_memrealtime() - st_t0;
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
                 st_a192 += active > 192 ? 1 : 0;
@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             tr[8] = (uint32_t)st_kit64;
             tr[9] = (uint32_t)st_kit128;
             tr[10] = (uint32_t)st_ev64;
-            tr[11] = (uint32_t)st_t64;
+            tr[11] = (uint32_t)st_refresh;
             tr[12] = (uint32_t)st_a192;
             tr[13] = (uint32_t)st_a128;
             tr[14] = (uint32_t)st_a64;

@@ -88,9 +88,9 @@ class Context:
                     wave_steps=int(a[8]), steps_any_need=int(a[9]), pixel_needs=int(a[10]))
 
     def draw_block_trace(self, blocks: int) -> np.ndarray:
-        """[blocks, 12] uint32 per draw block (gs_draw_block_trace): start, end (100 MHz ticks),
+        """[blocks, 16] uint32 per draw block (gs_draw_block_trace): start, end (100 MHz ticks),
         iterations, survivors, survivor steps, steps with a needing pixel, pixel needs, list
-        entries, steps while <= 64 / <= 128 pixels active, events while <= 64, ticks to <= 64,
+        entries, steps while <= 64 / <= 128 pixels active, events while <= 64, done-mask refreshes,
         dense-phase steps with > 192 / 129-192 / 65-128 active pixels, dense-phase events."""
         a = np.zeros((blocks, 16), np.uint32)
         n = lib().gs_draw_block_trace(self.handle, ptr(a), int(blocks))

@@ -58,12 +58,10 @@ for i in o:
 short = np.argsort(d)[:5]
 for i in short:
     print(f"  short block {i}: {d[i]:.1f} us  start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]} events {tr[i, 6]}")
-k64, k128, ev64, t64 = tr[:, 8].sum(), tr[:, 9].sum(), tr[:, 10].sum(), tr[:, 11]
+k64, k128, ev64, refr = tr[:, 8].sum(), tr[:, 9].sum(), tr[:, 10].sum(), tr[:, 11].sum()
 print(f"survivor steps {tr[:, 4].sum()}: with <=64 active px {k64} ({k64 / tr[:, 4].sum():.1%}), <=128 {k128}"
       f" ({k128 / tr[:, 4].sum():.1%}); events with <=64 active {ev64} ({ev64 / tr[:, 6].sum():.1%})")
-r = t64[t64 > 0] * 0.01
-print(f"blocks reaching <=64 active: {len(r)}; time to reach it / duration: "
-      f"{np.median(t64[t64 > 0] * 0.01 / d[t64 > 0]):.2f} (median)")
+print(f"done-mask refreshes (a pixel saturated): {refr} ({refr / max(1, tr[:, 12:15].sum()):.2f} per dense step)")
 a192, a128, a64, dev = (tr[:, k].sum() for k in (12, 13, 14, 15))
 nd = a192 + a128 + a64
 print(f"dense steps {nd}: >192 active {a192} ({a192 / nd:.1%}), 129-192 {a128} ({a128 / nd:.1%}), "
