@@ -102,6 +102,27 @@ def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags):
     assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{W}x{H}/image")
 
 
+@pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
+def test_non_finite_colours_match_oracle(ctx, oracle, flags):
+    """splats whose colour is +-inf or NaN (f_dc non-finite): the blend keeps a pixel by selects
+    when an event does not blend (a batch with a non-finite colour; `rgb * 0` would be NaN), and
+    the image still equals the oracle bit for bit"""
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    means, rot, sc, op, col = c2_scene(6_000, seed=77)
+    col = col.astype(np.float32).copy()
+    rng = np.random.default_rng(5)
+    bad = rng.choice(len(col), 300, replace=False)
+    col[bad[:100], 0] = np.inf
+    col[bad[100:200], 1] = -np.inf
+    col[bad[200:], 2] = np.nan
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, 640, 480, ctx=ctx)
+    assert not np.isfinite(sp.colours).all()
+    u = g.main_camera(640, 480).uniforms()
+    r = gpu_frame(sp, u, flags)
+    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags)
+    assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), "non-finite colours/image")
+
+
 def test_cull_is_exact_and_frames_deterministic(ctx):
     """the per-block cull never changes a pixel; repeated frames are bit-identical"""
     from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
