@@ -624,17 +624,17 @@ __global__ __launch_bounds__(kBlock) void k_bins_scan(uint32_t *__restrict__ cou
 // the 2x2 pixel quad at (2*(l%8), 2*(l/8)).  Sub-blocks never straddle coarse tiles, so
 // each pixel blends exactly its own tile's list (Q18 resolved).
 //
-// The tile's sorted list is consumed 64 entries per step through a four-stage register
-// pipeline (index load, box gather, box test + splat-data gather, blend; see k_draw), so
-// the loads of the next three steps are in flight while the current step blends.
-// Survivors are never staged in LDS: each stays in the registers of the lane that gathered
-// it and is broadcast with v_readlane while the wave walks the ballot mask in ascending
-// lane order -- exactly list order.  Per survivor, every lane evaluates power for its four
-// pixels; the pixels that can blend become (pixel, power) events, compacted and processed
-// one per lane on the pixel state kept in LDS (a pixel occurs at most once per survivor,
-// so events never conflict, and each pixel still sees its survivors in list order).  Each
-// pixel's arithmetic is the same sequence of IEEE ops as draw.glsl / the oracle, and the
-// filters only drop work draw.glsl would `continue` past (draw.glsl:118-126):
+// The tile's sorted list is consumed 64 entries per step through a three-stage register
+// pipeline (index load, box gather, box test; see k_draw); the box survivors queue in LDS in
+// list order, and batches of up to 64 are gathered one survivor per lane, culled exactly and
+// blended while the next chunks' loads are in flight.  A batch's survivors stay in the
+// registers of the lanes that gathered them and are broadcast with v_readlane while the wave
+// walks the batch mask in ascending lane order -- exactly list order.  Per survivor, every lane
+// evaluates power for its four pixels; the pixels that can blend become (pixel, power) events,
+// compacted and processed one per lane on the pixel state kept in LDS (a pixel occurs at most
+// once per survivor, so events never conflict, and each pixel still sees its survivors in list
+// order).  Each pixel's arithmetic is the same sequence of IEEE ops as draw.glsl / the oracle,
+// and the filters only drop work draw.glsl would `continue` past (draw.glsl:118-126):
 //   * box cull: the entry's alpha >= 1/255 box misses the sub-block;
 //   * exact cull: the alpha >= 1/255 ellipse misses the sub-block (ellipse_misses_rect);
 //   * pre-exp skip: power < ln(1/(255*o)) - 1e-3 implies alpha < 1/255 for any exp
@@ -726,12 +726,9 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
-// blend events compacted with exec-masked LDS writes (no spare entries): 5760 B of LDS per wave
-#ifndef GS_DRAW_MASKED_EV
-#define GS_DRAW_MASKED_EV 1
-#endif
+// 7 waves per SIMD: the LDS (5760 B per wave, events compacted by exec-masked writes) allows it
 #ifndef GS_DRAW_WAVES
-#define GS_DRAW_WAVES (GS_DRAW_MASKED_EV ? 7 : 6)
+#define GS_DRAW_WAVES 7
 #endif
 template <bool FAST_EXP, bool STATS>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVES))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
@@ -743,11 +740,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // pixel state, pixel id = 16*y + x in the sub-block; a pixel is done (:129-133) iff its
     // w >= 0.99 (pixels outside the image start at w = 1)
     __shared__ float4 s_col[256];
-    // one survivor's blend events: power and pixel id (split), entries 256 + lane take the
-    // writes of lanes without an event (5.6 KB of LDS per wave -> 7 waves/SIMD)
-    constexpr int kSpare = GS_DRAW_MASKED_EV ? 0 : 64;
-    __shared__ float s_epow[256 + kSpare];
-    __shared__ uint8_t s_epix[256 + kSpare];
+    // one survivor's blend events: power and pixel id (split); 5760 B of LDS per wave in all
+    // -> 7 waves/SIMD
+    __shared__ float s_epow[256];
+    __shared__ uint8_t s_epix[256];
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
@@ -831,12 +827,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // after a survivor saturated a pixel)
     uint64_t D0 = ballot(d00), D1 = ballot(d10), D2 = ballot(d01), D3 = ballot(d11);
     bool all_done = (D0 & D1 & D2 & D3) == ~0ull;
-    // v_cndmask on a uniform mask: m's lane bit set -> t, else f
-    auto sel_u32 = [](uint32_t f, uint32_t t, uint64_t m) {
-        uint32_t o;
-        asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(o) : "v"(f), "v"(t), "s"(m));
-        return o;
-    };
     // does a pixel of power p need the exp / blend path?  :118-126 continue on p > 0, plus the
     // pre-exp skip p < thr: p in [thr, 0] or NaN, as med3(p, thr, 0) == p or unordered (one
     // compare).  For thr > 0 (opacity < ~1/255) it admits p in [0, thr] instead, where
@@ -866,18 +856,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         const uint64_t A0 = ~D0, A1 = ~D1, A2 = ~D2, A3 = ~D3;
         const uint32_t a0 = (uint32_t)__popcll(A0), a1 = (uint32_t)__popcll(A1), a2 = (uint32_t)__popcll(A2);
         nact = a0 + a1 + a2 + (uint32_t)__popcll(A3);
-#if GS_DRAW_MASKED_EV
         if (__builtin_amdgcn_inverse_ballot_w64(A0)) s_epix[below(A0, 0)] = (uint8_t)(qbase + kQuad[0]);
         if (__builtin_amdgcn_inverse_ballot_w64(A1)) s_epix[below(A1, a0)] = (uint8_t)(qbase + kQuad[1]);
         if (__builtin_amdgcn_inverse_ballot_w64(A2)) s_epix[below(A2, a0 + a1)] = (uint8_t)(qbase + kQuad[2]);
         if (__builtin_amdgcn_inverse_ballot_w64(A3)) s_epix[below(A3, a0 + a1 + a2)] = (uint8_t)(qbase + kQuad[3]);
-#else
-        const uint32_t spare = 256u + (uint32_t)lane;
-        s_epix[((A0 >> lane) & 1) ? below(A0, 0) : spare] = (uint8_t)(qbase + kQuad[0]);
-        s_epix[((A1 >> lane) & 1) ? below(A1, a0) : spare] = (uint8_t)(qbase + kQuad[1]);
-        s_epix[((A2 >> lane) & 1) ? below(A2, a0 + a1) : spare] = (uint8_t)(qbase + kQuad[2]);
-        s_epix[((A3 >> lane) & 1) ? below(A3, a0 + a1 + a2) : spare] = (uint8_t)(qbase + kQuad[3]);
-#endif
         wave_lds_sync();
         spix = s_epix[min((uint32_t)lane, nact - 1)];
         SA = nact >= 64 ? ~0ull : ((1ull << nact) - 1);
@@ -1049,10 +1031,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             }
             if (nev != 0) {  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
-            // v_mbcnt); each pixel occurs at most once, so the events are independent.  Every
-            // lane writes each slot: lanes without that event into their own spare entry.
-#if GS_DRAW_MASKED_EV
-            // (exec-masked writes: the uniform masks are the branch conditions as they are)
+            // v_mbcnt); each pixel occurs at most once, so the events are independent.  The
+            // writes are exec-masked by the uniform event masks themselves (inverse ballot).
             if (__builtin_amdgcn_inverse_ballot_w64(b0)) {
                 const uint32_t e = below(b0, 0);
                 s_epow[e] = p00;
@@ -1073,29 +1053,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 s_epow[e] = p11;
                 s_epix[e] = (uint8_t)(qbase + kQuad[3]);
             }
-#else
-            const uint32_t spare = 256u + (uint32_t)lane;
-            {
-                const uint32_t e = sel_u32(spare, below(b0, 0), b0);
-                s_epow[e] = p00;
-                s_epix[e] = (uint8_t)(qbase + kQuad[0]);
-            }
-            {
-                const uint32_t e = sel_u32(spare, below(b1, e0), b1);
-                s_epow[e] = p10;
-                s_epix[e] = (uint8_t)(qbase + kQuad[1]);
-            }
-            {
-                const uint32_t e = sel_u32(spare, below(b2, e0 + e1), b2);
-                s_epow[e] = p01;
-                s_epix[e] = (uint8_t)(qbase + kQuad[2]);
-            }
-            {
-                const uint32_t e = sel_u32(spare, below(b3, e0 + e1 + e2), b3);
-                s_epow[e] = p11;
-                s_epix[e] = (uint8_t)(qbase + kQuad[3]);
-            }
-#endif
             wave_lds_sync();
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
