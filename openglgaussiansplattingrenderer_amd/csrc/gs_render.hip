@@ -727,6 +727,13 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #define GS_DRAW_BATCH 32
 #endif
 // 7 waves per SIMD: the LDS (5760 B per wave, events compacted by exec-masked writes) allows it
+// the exact cull of a batch runs from this many box survivors on (dense / sparse phase)
+#ifndef GS_CULL_DENSE
+#define GS_CULL_DENSE 3
+#endif
+#ifndef GS_CULL_SPARSE
+#define GS_CULL_SPARSE 6
+#endif
 #ifndef GS_DRAW_WAVES
 #define GS_DRAW_WAVES 7
 #endif
@@ -964,7 +971,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // exact cull of the survivors (uniform keep mask): it costs the wave the same for one
         // survivor as for 64 and drops about a third of them, so it runs from 3 survivors on
         // (same-box A/B: 1 -> 3 survivors, draw 0.335 -> 0.331 ms)
-        if (cull && __popcll(keep) >= 3)  // uniform
+        if (cull && __popcll(keep) >= GS_CULL_DENSE)  // uniform
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         // one exit (a uniform loop condition, no continue / return inside): fewer scalar
@@ -1098,7 +1105,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
 
     // sparse phase (see go_sparse): one pixel per lane, state in registers
     auto blend_sparse = [&](uint64_t keep, const SurvData &d, const SurvRgb &c) {
-        if (cull && __popcll(keep) >= 6)  // uniform (a sparse step costs less: from 6 survivors on)
+        if (cull && __popcll(keep) >= GS_CULL_SPARSE)  // uniform (a sparse step costs less: from 6 survivors on)
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         if (!keep) return;  // uniform
