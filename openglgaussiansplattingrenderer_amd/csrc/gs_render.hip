@@ -425,63 +425,99 @@ template <bool PACK>
 __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *__restrict__ keys,
                                                  uint32_t *__restrict__ vals, uint32_t cap,
                                                  uint32_t *__restrict__ phist) {
-    // 528 B of LDS: the owners' records come by ds_bpermute and the counts are 16-bit (with
+    // ~0.5 KB of LDS: the owners' records come by ds_bpermute and the counts are 16-bit (with
     // 5.6 KB it could not share a CU with seven waves of another frame's blend; measured
     // neutral either way, emit alone 0.0467 -> 0.0455 ms)
-    __shared__ uint32_t s_wave[kBlock / 64];
     __shared__ uint16_t s_incl[kBlock / 64][64];  // per wave: inclusive duplicate counts (<= 64 * 256)
     const uint2 off = fr.blocksum[blockIdx.x];
     const uint32_t V = fr.totals[0];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     uint32_t carry_m = off.x, carry_d = off.y;
-#pragma unroll 1
-    for (int it = 0; it < kPer; ++it) {
-        const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
-        int4 rc = make_int4(0, -1, -1, 0);
-        uint2 raw = make_uint2(0u, 0u);  // PACK: the record as stored
+    // Wave-major: wave w emits the workgroup's splats [256 w, 256 w + 256) as four items of 64
+    // consecutive splats, so one exchange of the waves' totals places every wave and each item
+    // then runs on wave scans alone (no workgroup barrier per item).  Entry order is unchanged:
+    // mains in splat order, duplicates splat-major.
+    const int wbase = blockIdx.x * kSplatsPerBlock + wid * (kPer * 64);
+    uint2 raws[kPer];
+    int4 rcs[kPer];
+    uint32_t ndup[kPer], incl_d[kPer];
+    uint64_t hasm[kPer];
+    uint32_t tot_m = 0, tot_d = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = wbase + j * 64 + lane;
+        raws[j] = make_uint2(0u, 0u);
+        rcs[j] = make_int4(0, -1, -1, 0);
         if (PACK) {
-            if (i < n) raw = reinterpret_cast<const uint2 *>(fr.rec)[i];
-            rc = unpack_rec(raw);
+            if (i < n) raws[j] = reinterpret_cast<const uint2 *>(fr.rec)[i];
         } else if (i < n) {
-            rc = fr.rec[i];
+            rcs[j] = fr.rec[i];
         }
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        if (PACK) rcs[j] = unpack_rec(raws[j]);
+        const int4 rc = rcs[j];
         const bool has = rc.y >= 0;
         const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
-        const int tileX = rc.y, tileY = rc.z;
-        uint32_t n_main = 0, n_dup = 0;
-        if (has) {
-            const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
-            const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
-            n_main = 1;
-            n_dup = (uint32_t)(rectCount - mainInRect);
-        }
-        // one scan of both: mains in the low 9 bits (<= 256 per item), duplicates above (<= 256
-        // per splat -- a main tile outside its rect, Q5, leaves the whole rect as duplicates --
-        // so <= 65536 per item, 23 bits)
-        uint32_t tp;
-        const uint32_t pp = block_excl_scan256(n_main | (n_dup << 9), s_wave, &tp);
-        const uint32_t pm = pp & 0x1ffu, pd = pp >> 9, t0 = tp & 0x1ffu, t1 = tp >> 9;
+        const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+        const int mainInRect = (rc.y >= minX && rc.y <= maxX && rc.z >= minY && rc.z <= maxY) ? 1 : 0;
+        ndup[j] = has ? (uint32_t)(rectCount - mainInRect) : 0u;
+        hasm[j] = __builtin_amdgcn_ballot_w64(has);
+        incl_d[j] = wave_incl_scan(ndup[j]);
+        tot_m += (uint32_t)__popcll(hasm[j]);
+        tot_d += (uint32_t)__builtin_amdgcn_readlane((int)incl_d[j], 63);
+    }
+    // the waves' totals -> each wave's offsets within the workgroup (one exchange)
+    __shared__ uint2 s_tot[kBlock / 64];
+    if (lane == 0) s_tot[wid] = make_uint2(tot_m, tot_d);
+    __syncthreads();
+    uint32_t wm = 0, wd = 0, all_m = 0, all_d = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint2 t = s_tot[w];
+        wm += w < wid ? t.x : 0u;
+        wd += w < wid ? t.y : 0u;
+        all_m += t.x;
+        all_d += t.y;
+    }
+    uint32_t run_m = off.x + wm, run_d = off.y + wd;
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+        // (the item's registers selected from the arrays by the uniform counter: no scratch)
+        int4 rc = rcs[0];
+        uint2 raw = raws[0];
+        uint32_t incl = incl_d[0];
+        uint64_t hm = hasm[0];
+#pragma unroll
+        for (int j = 1; j < kPer; ++j)
+            if (it == j) {
+                rc = rcs[j];
+                raw = raws[j];
+                incl = incl_d[j];
+                hm = hasm[j];
+            }
+        const int i = wbase + it * 64 + lane;
+        const bool has = rc.y >= 0;
         if (has) {
             // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
-            const uint32_t mpos = carry_m + pm;
-            const uint32_t tileIndex = (uint32_t)tileY * 16u + (uint32_t)tileX;
+            const uint32_t mpos = run_m + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+            const uint32_t tileIndex = (uint32_t)rc.z * 16u + (uint32_t)rc.y;
             if (mpos < cap) {
                 keys[mpos] = f2u((float)tileIndex + u2f((uint32_t)rc.x));
                 vals[mpos] = (uint32_t)i;
             }
         }
-        // this wave's duplicates: [V + carry_d + pd0, + T)
-        const uint32_t pd0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)pd);
-        const uint32_t incl = pd - pd0 + n_dup;
+        run_m += (uint32_t)__popcll(hm);
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (T) {  // uniform per wave
+        if (T) {  // uniform per wave: this item's duplicates [V + run_d, + T)
             s_incl[wid][lane] = (uint16_t)incl;
             wave_sync_lds();
-            const uint32_t d0 = V + carry_d + pd0;
+            const uint32_t d0 = V + run_d;
             const uint32_t room = cap > d0 ? cap - d0 : 0u;  // entries of this range that fit
             uint32_t *kd = keys + d0;
             uint32_t *vd = vals + d0;
-            const int ibase = blockIdx.x * kSplatsPerBlock + it * kBlock + wid * 64;
+            const int ibase = wbase + it * 64;
             const uint32_t lim = min(T, room);  // entries to write
             // uniform trip count (lanes past the end compute a harmless owner, store nothing)
             for (uint32_t e0 = 0; e0 < T; e0 += 64) {
@@ -500,9 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
                 const bool mainIn = r.y >= rx0 && r.y <= rx1 && r.z >= ry0 && r.z <= ry1;
                 const uint32_t mpos_walk = (uint32_t)((r.z - ry0) * w + (r.y - rx0));
                 const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
-                // k / w for k < 256, 1 <= w <= 16: (k + 1/2) / w is at least 1/32 from an integer,
-                // far beyond the rounding of v_rcp and the product, so the truncation is exact
-                // (w <= 0 only for lanes past the range's end, which store nothing)
+                // k / w for k < 256, 1 <= w <= 16 (see below)
                 const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(w, 1)));
                 const uint32_t dx = k - dy * (uint32_t)w;
                 const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
@@ -513,9 +547,10 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
             }
             wave_sync_lds();  // s_incl is rewritten by the next item
         }
-        carry_m += t0;
-        carry_d += t1;
+        run_d += T;
     }
+    carry_m = off.x + all_m;
+    carry_d = off.y + all_d;
     // prefix sort (gs_internal.hpp): the emitted keys at positions j * kPrefixSample of this
     // workgroup's two output ranges go to the sampled histogram (copy j % kPrefixHistCopies) --
     // after the loop, so no load of it waits behind these atomics
