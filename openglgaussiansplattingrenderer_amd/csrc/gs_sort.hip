@@ -27,7 +27,10 @@ namespace {
 
 constexpr int kItems = 16;                    // keys per lane
 constexpr int kWaveTile = 64 * kItems;        // 1024 keys per wave
-constexpr int kWaveSmall = 4, kWaveBig = 8;   // waves per workgroup: passes 1-3 / pass 0
+#ifndef GS_WAVE_SMALL
+#define GS_WAVE_SMALL 4
+#endif
+constexpr int kWaveSmall = GS_WAVE_SMALL, kWaveBig = 8;   // waves per workgroup: passes 1-3 / pass 0
 constexpr int kTileSmall = kWaveSmall * kWaveTile;  // 4096
 constexpr int kRadix = 256;
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
@@ -146,6 +149,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
                                                     uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ tile_counts, PrefixDev pre) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems;
+    static_assert(kThreads >= kRadix, "one thread per digit flushes the counts");
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
     const uint32_t tile = xcd_tile(live);
@@ -444,6 +448,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
                                                       const uint32_t *__restrict__ hist, uint32_t nb,
                                                       const uint32_t *__restrict__ row_total, PrefixDev pre) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
+    static_assert(kThreads >= kRadix, "one thread per digit scans the counts");
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
     const uint32_t tile = xcd_tile(live);
