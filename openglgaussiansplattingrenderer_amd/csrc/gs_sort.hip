@@ -30,7 +30,10 @@ constexpr int kWaveTile = 64 * kItems;        // 1024 keys per wave
 #ifndef GS_WAVE_SMALL
 #define GS_WAVE_SMALL 4
 #endif
-constexpr int kWaveSmall = GS_WAVE_SMALL, kWaveBig = 8;   // waves per workgroup: passes 1-3 / pass 0
+#ifndef GS_WAVE_BIG
+#define GS_WAVE_BIG 8
+#endif
+constexpr int kWaveSmall = GS_WAVE_SMALL, kWaveBig = GS_WAVE_BIG;   // waves per workgroup: passes 1-3 / pass 0
 constexpr int kTileSmall = kWaveSmall * kWaveTile;  // 4096
 constexpr int kRadix = 256;
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
