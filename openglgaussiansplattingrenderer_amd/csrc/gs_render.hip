@@ -758,6 +758,9 @@ struct alignas(16) SurvRgb {
 };
 static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw");
 
+#ifndef GS_DRAW_POWPIX
+#define GS_DRAW_POWPIX 1
+#endif
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
@@ -784,7 +787,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     __shared__ float4 s_col[256];
     // one survivor's blend events: power and pixel id (split); 5760 B of LDS per wave in all
     // -> 7 waves/SIMD
-    __shared__ float s_epow[256];
+    __shared__ __attribute__((aligned(16))) float s_epow[256];
     __shared__ uint8_t s_epix[256];
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
@@ -1075,24 +1078,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             // compact this survivor's blend events (slot k's after slots < k, lane order via
             // v_mbcnt); each pixel occurs at most once, so the events are independent.  The
             // writes are exec-masked by the uniform event masks themselves (inverse ballot).
+#if GS_DRAW_POWPIX
+            // the powers go to their pixels' slots (every lane, two 8-byte stores, no address
+            // arithmetic); the compaction lists only the event pixels
+            *reinterpret_cast<float2 *>(&s_epow[qbase]) = make_float2(p00, p10);
+            *reinterpret_cast<float2 *>(&s_epow[qbase + 16u]) = make_float2(p01, p11);
+#endif
             if (__builtin_amdgcn_inverse_ballot_w64(b0)) {
                 const uint32_t e = below(b0, 0);
+#if !GS_DRAW_POWPIX
                 s_epow[e] = p00;
+#endif
                 s_epix[e] = (uint8_t)(qbase + kQuad[0]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b1)) {
                 const uint32_t e = below(b1, e0);
+#if !GS_DRAW_POWPIX
                 s_epow[e] = p10;
+#endif
                 s_epix[e] = (uint8_t)(qbase + kQuad[1]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b2)) {
                 const uint32_t e = below(b2, e0 + e1);
+#if !GS_DRAW_POWPIX
                 s_epow[e] = p01;
+#endif
                 s_epix[e] = (uint8_t)(qbase + kQuad[2]);
             }
             if (__builtin_amdgcn_inverse_ballot_w64(b3)) {
                 const uint32_t e = below(b3, e0 + e1 + e2);
+#if !GS_DRAW_POWPIX
                 s_epow[e] = p11;
+#endif
                 s_epix[e] = (uint8_t)(qbase + kQuad[3]);
             }
             wave_lds_sync();
@@ -1102,7 +1119,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             auto event = [&](uint32_t e) {
                 // straight line: the pixel's state is loaded with the event, before the exp
                 const uint32_t pix = s_epix[e];
-                const float power = s_epow[e];
+                const float power = s_epow[GS_DRAW_POWPIX ? pix : e];
                 float4 col = s_col[pix];
                 const float ex = FAST_EXP ? __expf(power) : exp_defined_event(power);
                 const float alpha = fminf(0.99f, ex * o);
