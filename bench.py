@@ -169,9 +169,50 @@ def sort_bench(ctx, reps: int = 50, warm: int = 5):
             ms_pairs.append(t)
     med = float(np.median(ms))
     medp = float(np.median(ms_pairs))
-    return dict(n=SORT_N, ms_argsort=med, gkeys_per_s=SORT_N / med / 1e6, ms_pairs=medp,
-                gkeys_per_s_pairs=SORT_N / medp / 1e6,
-                hbm_frac_pairs=68.0 * SORT_N / (medp * 1e-3) / 1e9 / HBM_PEAK_GBS, sorted_ok=ok)
+    out = dict(n=SORT_N, ms_argsort=med, gkeys_per_s=SORT_N / med / 1e6, ms_pairs=medp,
+               gkeys_per_s_pairs=SORT_N / medp / 1e6,
+               hbm_frac_pairs_cache_resident=68.0 * SORT_N / (medp * 1e-3) / 1e9 / HBM_PEAK_GBS,
+               cache_resident_note="5.12M pairs = 41 MB (82 MB with the alternate buffers) sit inside the 256 MiB "
+                                   "Infinity Cache: an L2/MALL figure, not an HBM one",
+               sorted_ok=ok)
+    del kb, ob, k2, v2
+    out["beyond_cache"] = sort_bench_big(ctx)
+    return out
+
+
+SORT_BIG_N = 64 << 20  # 64M pairs: 512 MB of (key, value), 1.28 GB with the alternate buffers
+
+
+def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
+    """The same pair sort beyond the caches: 64M uniform 32-bit keys (HBM-resident), median of
+    `reps` hipEvent-timed sorts; algorithmic bytes 68 B/key; counter-based bytes from
+    the committed rocprofv3 calibration (profiles/r02/calibration.txt: 88.1 B/key measured by
+    FETCH_SIZE x2 + WRITE_SIZE at this size)."""
+    import openglgaussiansplattingrenderer_amd as g
+    n = SORT_BIG_N
+    rng = np.random.default_rng(64)
+    keys = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    vals = np.arange(n, dtype=np.uint32)
+    kb = g.DeviceBuffer.from_array(ctx, keys)
+    vb = g.DeviceBuffer.from_array(ctx, vals)
+    ms = []
+    for i in range(warm + reps):
+        kb.upload(keys)
+        vb.upload(vals)
+        g.sort_pairs(ctx, kb, vb, n)
+        t = ctx.last_kernel_ms(g.GS_KERNEL_SORT)
+        if i >= warm:
+            ms.append(t)
+    k_out = kb.download(np.uint32, n)
+    ok = bool(np.all(k_out[1:] >= k_out[:-1]))
+    med = float(np.median(ms))
+    b_counter = 88.1  # B/key, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r02/calibration.txt)
+    return dict(n=n, keys="uniform 32-bit, seeded", ms_pairs=round(med, 4), gkeys_per_s=round(n / med / 1e6, 2),
+                hbm_frac_algorithmic=round(68.0 * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                hbm_frac_counters=round(b_counter * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                counter_bytes_per_key=b_counter, sorted_ok=ok,
+                source="hipEvents around gs_sort_pairs_u32 (12 kernels); 68 B/key algorithmic, 88.1 B/key by "
+                       "counters (profiles/r02/calibration.txt)")
 
 
 def cpu_baseline(sp, u, flags, budget_s: float = 20.0):
@@ -255,6 +296,8 @@ def main():
                          "emission / sort with frame k's blend, 3 (default here) also the blends' tails")
     ap.add_argument("--view", type=int, default=None,
                     help="C5 pose index to render (default: this rank's, main pose + rotateRight(45 deg * k))")
+    ap.add_argument("--draw-sub", type=int, default=0, choices=(0, 8, 16),
+                    help="the blend's sub-block form (gs_ctx_set_draw_sub): 0 by entry count (default), 8, 16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
@@ -300,6 +343,7 @@ def main():
     ndev = max(1, ndev.value)
     ctx = g.Context(local % ndev)
     ctx.set_lanes(args.lanes)
+    ctx.set_draw_sub(args.draw_sub)
     sp, data_desc = load_scene(args.config, W, H, ctx, flags)
     if args.sh:
         rng = np.random.default_rng(4242)
@@ -371,40 +415,54 @@ def main():
     # per-stage average device time over the timed frames (hipEvents on the ctx stream)
     nf = max(1, tm["frames"])
     stage_ms = {k[3:]: tm[k] / nf for k in ("ms_preprocess", "ms_emit", "ms_sort", "ms_bins", "ms_draw")}
-    # algorithmic bytes per launch, fp32 SoA, 4-B payload
+    # algorithmic bytes per launch, fp32 SoA, 4-B payload; a prefix-sorted frame's
+    # sort: 4 B/entry (pass-0 key read for the histograms) + 16 B/entry (pass-0 pairs in and the
+    # kept pairs out, charged at every entry) + 48 B per kept entry (passes 1-3), else 68 B/entry
+    kept = int(ps["kept"]) if ps["frames"] and ps["entries"] == E else 0
+    sort_bytes = 4 * E + 16 * E + 48 * kept if kept else 68 * E
     alg = {
         "preprocess": 40 * N + 24 * V,
         "emit": 8 * E,
-        "sort": 68 * E,
+        "sort": sort_bytes,
         "bins": 4 * E + 1024,
         "draw": 40 * E + 4 * W * H,
     }
     draw_ms_live = tm_draw["ms_draw"] / max(1, tm_draw["frames"])  # timed region, HIP events
-    # the dominant kernel: the blend (the longest stage alone; with ranks sharing one GPU the
-    # stage-timing pass overlaps other ranks' work, so this is not re-derived per run)
-    dom = "draw"
-    if dom == "draw":
-        stage_ms_dom = draw_ms_live
+    one_ms = tm_serial["ms_draw"] / max(1, tm_serial["frames"])    # frames one at a time
+    # the dominant kernel: the longest stage of the one-lane stage pass (one rank per GPU); with
+    # ranks sharing a GPU that pass overlaps other ranks' work, so the blend is taken as measured
+    # on a GPU of its own in round 2 (profiles/r02: k_draw is the longest kernel at every config)
+    if world <= ndev:
+        dom = max(("preprocess", "emit", "sort", "draw"), key=lambda k: stage_ms[k])
+        dom_source = "longest stage of the one-lane stage-timing pass"
     else:
-        stage_ms_dom = stage_ms[dom]
+        dom = "draw"
+        dom_source = "fixed to the blend: ranks share a GPU, so the stage pass is not one kernel's time"
     kern_name = {"preprocess": "k_preprocess", "emit": "k_emit", "sort": "k_downsweep", "bins": "k_bins_count",
                  "draw": "k_draw"}[dom]
+    # avg_launch_ms: the kernel with the GPU to itself (frames one at a time, hipEvents on its own
+    # dispatch) -- what a rocprofv3 kernel trace of the one-lane pass reports for it
+    # (profiles/r03/); the timed region's launches share the GPU with the other frames' kernels and
+    # are reported beside it
+    stage_ms_dom = one_ms if dom == "draw" else stage_ms[dom]
     achieved = alg[dom] / (stage_ms_dom * 1e-3) / 1e9
-    roofline = {"bound": "hbm", "kernel": kern_name, "stage": dom, "achieved": round(achieved, 2),
+    roofline = {"bound": "hbm", "kernel": kern_name, "stage": dom, "dominant_source": dom_source,
+                "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": int(alg[dom]), "avg_launch_ms": round(stage_ms_dom, 4),
-                "avg_launch_ms_source": ("hipEvents on the draw dispatch over the timed frames" +
-                                         (" (sharing the GPU with the next frame's stages)" if args.lanes > 1 else "")
-                                         if dom == "draw" else "hipEvents of the stage-timing pass"),
+                "avg_launch_ms_source": ("hipEvents on the draw dispatch, frames one at a time (1 lane): the kernel "
+                                         "alone on the GPU" if dom == "draw" else
+                                         "hipEvents of the one-lane stage-timing pass"),
                 "traffic": load_pmc(kern_name)}
-    if dom == "draw":  # the same kernel with the GPU to itself (the one-lane pass): its own roofline
-        one_ms = tm_serial["ms_draw"] / max(1, tm_serial["frames"])
-        one = alg["draw"] / (one_ms * 1e-3) / 1e9
-        roofline["one_frame"] = {"avg_launch_ms": round(one_ms, 4), "achieved": round(one, 2),
-                                 "frac": round(one / HBM_PEAK_GBS, 4),
-                                 "source": "hipEvents on the draw dispatch, frames one at a time (1 lane)"}
+    if dom == "draw":
+        live = alg["draw"] / (draw_ms_live * 1e-3) / 1e9
+        roofline["timed_region"] = {
+            "avg_launch_ms": round(draw_ms_live, 4), "achieved": round(live, 2), "frac": round(live / HBM_PEAK_GBS, 4),
+            "source": "hipEvents on the draw dispatch over the timed frames" +
+                      (f" ({args.lanes} frames in flight: the blend shares the GPU with other frames' kernels, "
+                       "so this span is longer than the kernel's own time)" if args.lanes > 1 else "")}
         roofline["issue"] = issue_ceiling(kern_name, one_ms)
-    frame_bytes = 40 * N + 24 * V + 120 * E + 4 * W * H
+    frame_bytes = alg["preprocess"] + alg["emit"] + alg["sort"] + alg["draw"]  # bins ride on the sort's first pass
     frame_frac = frame_bytes * (args.steps / local_s) / 1e9 / HBM_PEAK_GBS
 
     # per-rank (view, entries, time) to rank 0 (gloo, host side)
@@ -447,10 +505,14 @@ def main():
                       "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
                       "stage_ms_source": f"{nser} frames one at a time (1 lane) with every stage boundary timed, before the timed region",
                       "frames_in_flight": args.lanes,
+                      "draw_sub_block": ctx.set_draw_sub(),
                       "serial_ms_per_frame": round(serial_ms, 4),
                       "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
                       "prefix_sort": prefix,
-                      "frame_hbm_frac_algorithmic": round(frame_frac, 4)},
+                      "frame_bytes_algorithmic": int(frame_bytes),
+                      "frame_hbm_frac_algorithmic": round(frame_frac, 4),
+                      "frame_bytes_source": "40N + 24V (preprocess) + 8E (emission) + sort (4E + 16E + 48 kept "
+                                            "when prefix-sorted, else 68E) + 40E + 4WH (blend)"},
             "host": host,
             "ranks": ranks,
             "roofline": roofline,

@@ -103,10 +103,22 @@ int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
  * `target` entries deep (default 32768; the blend reads ~2-20k of lists up to 0.8M long at
  * C3) and the rest of it is left unsorted.  Images are unchanged: a frame whose blend reaches
  * an unsorted position before saturating is rendered again with the full sort, and the target
- * doubles for the frames after it.  target 0: always the full sort.  Frames with fewer than
+ * doubles for the frames after it; after 64 frames in a row without a miss it halves again,
+ * never below the configured target.  target 0: always the full sort.  Frames with fewer than
  * 64 * target entries (the previous frame's count) use the full sort.  Returns the current
  * target in *current when it is not NULL (with target < 0: only that). */
 int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current);
+/* The blend's sub-block form (beyond the reference, whose draw.glsl runs 32x32 workgroups,
+ * src/Splats.cpp:378): 16 = one wave per 16x16 pixels, each lane a 2x2 quad (throughput form:
+ * large frames); 8 = one wave per 8x8 pixels, one pixel per lane (latency form: four times the
+ * waves, for frames whose blend is bound by its longest sub-block); 0 (default) = 8 for frames
+ * with fewer than 2^21 entries, else 16; -1 leaves it.  Images are identical in every form.
+ * *current (when not NULL) receives the form the newest frame's blend used. */
+int gs_ctx_set_draw_sub(gs_ctx *ctx, int sub, int *current);
+/* The small-frame forms: frames whose entry count (the newest one seen) is below draw_entries
+ * blend in 8x8 sub-blocks when gs_ctx_set_draw_sub is 0 (default 2^21), and below sort_entries
+ * sort in 8 launches instead of 12 (default 2^19).  A negative value leaves a limit. */
+int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entries);
 /* prefix-sort counters: [0] frames prefix-sorted, [1] of them rendered again (a blend reached
  * an unsorted position), [2] entries kept by the newest retired prefix-sorted frame, [3] its
  * entry count; reset != 0 clears [0] and [1] */

@@ -14,7 +14,9 @@
 #include <cstdint>
 #include <cstring>
 #include <iostream>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "gsplat.h"
@@ -39,22 +41,40 @@ inline int report(int rc, const gs_ctx *ctx = nullptr) {
 
 // One GPU: replaces the GL context + compiled programs.  Like a GL context it can be made
 // current on the calling thread (the first one created is), so the reference's context-free
-// calls -- GPURadixSort's 10-argument form -- find it.
+// calls -- GPURadixSort's 10-argument form -- find it.  A thread's current Context is held as
+// (pointer, serial) and checked against a process-wide registry of live contexts, so a Context
+// destroyed on another thread (or a new one at the same address) is never returned.
 class Context {
   public:
     explicit Context(int device = 0) {
         report(gs_ctx_create(device, &ctx_));
-        if (!current_slot()) current_slot() = this;
+        {
+            std::lock_guard<std::mutex> g(registry_mutex());
+            serial_ = ++serial_counter();
+            registry()[this] = serial_;
+        }
+        if (!current()) makeCurrent();
     }
     ~Context() {
-        if (current_slot() == this) current_slot() = nullptr;
+        {
+            std::lock_guard<std::mutex> g(registry_mutex());
+            registry().erase(this);
+        }
+        if (current_slot().ctx == this) current_slot() = Slot{};
         gs_ctx_destroy(ctx_);
     }
     Context(const Context &) = delete;
     Context &operator=(const Context &) = delete;
     gs_ctx *get() const { return ctx_; }
-    void makeCurrent() { current_slot() = this; }          // glfwMakeContextCurrent
-    static Context *current() { return current_slot(); }    // or null
+    void makeCurrent() { current_slot() = Slot{this, serial_}; }  // glfwMakeContextCurrent
+    // the calling thread's current Context, or null (none made current, or it was destroyed)
+    static Context *current() {
+        const Slot s = current_slot();
+        if (!s.ctx) return nullptr;
+        std::lock_guard<std::mutex> g(registry_mutex());
+        const auto it = registry().find(s.ctx);
+        return (it != registry().end() && it->second == s.serial) ? s.ctx : nullptr;
+    }
     void finish() const { report(gs_sync(ctx_), ctx_); }  // glFinish
     // frames in flight on the device: 2 (default; frame k+1's preprocess / emission / sort
     // overlap frame k's blend), 3 (one more in flight), or 1 (one frame at a time, as
@@ -62,11 +82,28 @@ class Context {
     int setLanes(int lanes) const { return report(gs_ctx_set_lanes(ctx_, lanes), ctx_); }
 
   private:
-    static Context *&current_slot() {
-        static thread_local Context *cur = nullptr;
+    struct Slot {
+        Context *ctx = nullptr;
+        uint64_t serial = 0;
+    };
+    static Slot &current_slot() {
+        static thread_local Slot cur;
         return cur;
     }
+    static std::mutex &registry_mutex() {
+        static std::mutex m;
+        return m;
+    }
+    static std::unordered_map<const Context *, uint64_t> &registry() {
+        static std::unordered_map<const Context *, uint64_t> r;
+        return r;
+    }
+    static uint64_t &serial_counter() {
+        static uint64_t c = 0;
+        return c;
+    }
     gs_ctx *ctx_ = nullptr;
+    uint64_t serial_ = 0;
 };
 
 // src/sort.cpp:15-124 -- kernels are built ahead of time; nothing to compile.

@@ -21,6 +21,24 @@
 // 4 sort start, 5 sort done, 6 bins done, 7 draw start, 8 draw done
 constexpr int kEv = 9;
 constexpr int kRing = 4;
+constexpr int kPrefixDecay = 64;  // frames without a prefix-sort miss before the depth halves
+// Frames with fewer entries than this, and at most kSmallDrawSubBlocks 16x16 sub-blocks, blend
+// in 8x8 sub-blocks (gs_ctx_set_draw_sub): their blend is latency-bound (~one wave per SIMD, the
+// longest sub-block running ~200 survivor steps), and four times the waves, each a quarter of
+// the pixels, shorten it (C2: 0.134 -> 0.048 ms).  With more sub-blocks the 16x16 form wins even
+// for few entries (1080p C5 views of 0.16-0.96M entries: 0.14-0.24 ms against 0.17-0.39).
+constexpr int64_t kSmallDrawEntries = 2 << 20;
+constexpr int64_t kSmallDrawSubBlocks = 2048;
+// Scenes of at most this many preprocess workgroups (1024 splats each) run preprocess and
+// emission fused (k_pre_emit, one launch instead of three).  Larger scenes keep the three
+// kernels: the fused kernel's look-back chain (each co-resident workgroup walks back to the
+// newest inclusive prefix, a cross-XCD round trip of ~2-3 us per 64 workgroups under the
+// streaming load) cost more than the emission record round trip it saves (C3: 0.184 against
+// 0.152 ms).
+constexpr int kFusedMaxBlocks = 64;
+// ... and sort in 8 launches instead of 12 (k_sweep_small: each sweep sums its histogram rows
+// itself, which costs a round trip per 64 tiles of 4096 entries)
+constexpr int64_t kSmallSortEntries = 512 << 10;
 
 // A frame lane: a stream and the per-frame buffers of the frames it runs.  Consecutive frames
 // alternate between the ctx's lanes (two by default), so frame k+1's preprocess, emission and
@@ -45,6 +63,16 @@ struct Lane {
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     bool vals_partial = false;  // the frame was prefix-sorted: vals holds only each list's sorted prefix
     uint32_t *pre_buf = nullptr;  // prefix-sort state (gs::kPrefixWords words, see gs::PrefixDev)
+    // k_pre_emit's look-back state: two halves of cap_blocks status words, alternate frames of
+    // this lane use alternate halves (lb_par); zero on allocation
+    uint64_t *lb = nullptr;
+    uint32_t lb_cap = 0;  // status words per half
+    int lb_par = 0;
+    bool split = false;  // the newest frame's entries are in the split layout (k_pre_emit)
+    // the newest frame's scene and preprocess parameters (a split frame's readbacks preprocess it
+    // again on the staged path, which also writes the emission records)
+    const gs_scene *pe_scene = nullptr;
+    gs::PreParams pe_P{};
     gs::SortScratch sort;
     // bins
     uint32_t *bin_counts = nullptr;  // [256]
@@ -95,7 +123,10 @@ struct gs_ctx {
         const void *draw_out = nullptr;
         bool drawn = false, draw_stats = false;
         bool prefix = false;  // prefix-sorted: its blend may flag a miss (ring word 2)
+        bool fused = false;   // k_pre_emit: split entry layout (needs n + D entries), no emission event
+        int n = 0;
         uint32_t cap_sel = 0;  // prefix-sorted: the kept entries its sort passes 1-3 could hold
+        int target = 0;        // prefix-sorted: its depth
     };
     Slot slot[kRing];
     hipEvent_t ev[kRing][kEv] = {};
@@ -112,8 +143,21 @@ struct gs_ctx {
     gs_timing acc = {};
     bool in_render = false;      // inside gs_render: host waits count as ms_host_wait
     // prefix sort (gs_ctx_set_sort_prefix)
+    // the depth: prefix_base as configured; a miss doubles prefix_target, and every kPrefixDecay
+    // frames in a row without one halve it again, down to prefix_base (one close-up or scene
+    // swap does not deepen the sort -- or turn it off -- for good)
+    int prefix_base = 32768;
     int prefix_target = 32768;
+    int prefix_clean_run = 0;
     uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
+    int prefix_kept_target = 0;  // the depth the frame of prefix_kept was sorted to
+    // the blend's sub-block form (gs_ctx_set_draw_sub): 0 by the frame's entry count, 8 or 16
+    int draw_sub = 0;
+    int last_draw_sub = 0;  // the newest frame's
+    // the small-frame forms (gs_ctx_set_small_limits): frames with fewer entries (the newest count
+    // seen) blend in 8x8 sub-blocks (draw_sub 0) and sort in 8 launches (k_sweep_small)
+    int64_t small_draw_entries = kSmallDrawEntries;
+    int64_t small_sort_entries = kSmallSortEntries;
 };
 
 struct gs_scene {
@@ -210,8 +254,13 @@ int ensure_splats(gs_ctx *ctx, int n) {
     const int nb = gs::preprocess_blocks(cap);
     int rc;
     if ((rc = grow(ctx, ctx->L->sd, cap)) || (rc = grow(ctx, ctx->L->cullbox, cap)) ||
-        (rc = grow(ctx, ctx->L->rec, cap)) || (rc = grow(ctx, ctx->L->blocksum, nb)))
+        (rc = grow(ctx, ctx->L->rec, cap)) || (rc = grow(ctx, ctx->L->blocksum, nb)) ||
+        (rc = grow(ctx, ctx->L->lb, 2 * (size_t)nb)))
         return rc;
+    // (ordered on the lane's stream with the kernels that use it)
+    GS_HIP(ctx, hipMemsetAsync(ctx->L->lb, 0, 2 * (size_t)nb * sizeof(uint64_t), ctx->L->stream));
+    ctx->L->lb_cap = (uint32_t)nb;
+    ctx->L->lb_par = 0;
     ctx->L->n_cap = cap;
     return GS_OK;
 }
@@ -222,8 +271,10 @@ int ensure_entries(gs_ctx *ctx, int64_t e) {
     int rc;
     if ((rc = grow(ctx, ctx->L->keys, (size_t)cap)) || (rc = grow(ctx, ctx->L->vals_base, (size_t)cap + gs::kValsPad)))
         return rc;
-    // the words before vals stay zero (nothing writes them): splat 0 for k_draw's culled entries
-    GS_HIP(ctx, hipMemset(ctx->L->vals_base, 0, gs::kValsPad * 4));
+    // the words before vals stay zero (nothing writes them): splat 0 for k_draw's culled entries;
+    // the rest is zeroed too, so every word a kernel could read before it is written is a valid id
+    GS_HIP(ctx, hipMemsetAsync(ctx->L->vals_base, 0, ((size_t)cap + gs::kValsPad) * 4, ctx->L->stream));
+    GS_HIP(ctx, hipMemsetAsync(ctx->L->keys, 0, (size_t)cap * 4, ctx->L->stream));
     ctx->L->vals = ctx->L->vals_base + gs::kValsPad;
     ctx->L->e_cap = cap;
     return GS_OK;
@@ -268,7 +319,7 @@ void accumulate(gs_ctx *ctx, int set) {
     if (ctx->timing_mode >= 1) ctx->acc.ms_draw += elapsed(e[7], e[8]);
     if (ctx->timing_mode < 2) return;
     ctx->acc.ms_preprocess += elapsed(e[0], e[1]);
-    ctx->acc.ms_emit += elapsed(e[2], e[3]);
+    if (!ctx->slot[set].fused) ctx->acc.ms_emit += elapsed(e[2], e[3]);  // (fused: in the preprocess)
     ctx->acc.ms_sort += elapsed(e[4], e[5]);
     ctx->acc.ms_bins += elapsed(e[5], e[6]);
     ctx->acc.ms_frame += elapsed(e[0], e[8]);
@@ -337,11 +388,22 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
             if (sl.prefix) {
                 ctx->prefix_kept = ctx->h_ring[4 * k + 3];
+                ctx->prefix_kept_target = sl.target;
                 ctx->prefix_E = (uint64_t)(V + D);
             }
-            if (miss) ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
+            if (miss) {
+                ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
+                ctx->prefix_clean_run = 0;
+            } else if (++ctx->prefix_clean_run >= kPrefixDecay) {  // (prefix-sorted or not: a depth that
+                // turned the prefix sort off, E < 64 * target, comes down again too)
+                ctx->prefix_clean_run = 0;
+                if (ctx->prefix_target > ctx->prefix_base)
+                    ctx->prefix_target = std::max(ctx->prefix_base, ctx->prefix_target / 2);
+            }
             if (miss || full) ctx->prefix_redo += 1;
-            if (V + D > sl.cap || miss || full) return handle_overflow(ctx);
+            // the split layout of a fused frame holds its duplicates from index n on
+            const int64_t need = sl.fused ? (int64_t)sl.n + D : V + D;
+            if (need > sl.cap || miss || full) return handle_overflow(ctx);
             ctx->V = V;
             ctx->D = D;
             ctx->E = V + D;
@@ -465,7 +527,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
         void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
-                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf};
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
@@ -769,6 +831,8 @@ void gs_scene_destroy(gs_scene *scene) {
         (void)hipSetDevice(ctx->device);
         (void)gs_sync(ctx);  // frames in flight (and their re-renders) may read the scene
         ctx->scenes.erase(std::remove(ctx->scenes.begin(), ctx->scenes.end(), scene), ctx->scenes.end());
+        for (Lane &ln : ctx->lane)
+            if (ln.pe_scene == scene) ln.pe_scene = nullptr;
     }
     if (scene->soa) (void)hipFree(scene->soa);
     if (scene->colour) (void)hipFree(scene->colour);
@@ -812,6 +876,10 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
     return use_device(ctx);
 }
 
+// covariance loads only for the splats inside the NDC square when the newest frame seen had most
+// of the scene's splats culled (the small C5 views)
+bool lazy_loads(const gs_ctx *ctx, int n) { return ctx->n == n && ctx->e_known && ctx->V * 2 < (int64_t)n; }
+
 // preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->L->totals
 int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {
     const int n = scene->n;
@@ -834,10 +902,50 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = gs::preprocess_blocks(n);
     // k_scan_blocksums writes (V, D) to ctx->L->totals and to this slot's pinned host copy
-    gs::launch_preprocess(ctx->L->stream, P, scene_dev(scene), fr, fev(ctx, 0));
+    gs::launch_preprocess(ctx->L->stream, P, scene_dev(scene), fr, fev(ctx, 0), lazy_loads(ctx, n));
     gs::launch_scan_blocksums(ctx->L->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
+    ctx->L->split = false;
+    ctx->L->pe_scene = scene;
+    ctx->L->pe_P = P;
+    return GS_OK;
+}
+
+// The fused preprocess + emission of a frame enqueued without a host round trip (k_pre_emit,
+// events 0 and 1): entries in the split layout (duplicates from index n), (V, D) on the device
+// and in the slot's pinned copy.  prefix_hist: the prefix sort's sampled histogram, or null.
+int enqueue_pre_emit(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
+                     uint32_t *prefix_hist) {
+    const int n = scene->n;
+    const bool sh = (flags & GS_FLAG_SH) != 0;
+    if (sh && !scene->sh) return set_error(ctx, GS_ERR_INVALID, "GS_FLAG_SH: the scene has no SH (gs_scene_set_sh)");
+    if (int rc = ensure_splats(ctx, n)) return rc;
+    if (sh && ctx->L->col_cap < n) {
+        if (int rc = grow(ctx, ctx->L->col, (size_t)n)) return rc;
+        ctx->L->col_cap = n;
+    }
+    if (int rc = begin_frame(ctx)) return rc;
+    ctx->flags = flags;
+    gs::PreParams P = pre_params(u, flags, n);
+    P.sh = sh ? 1 : 0;
+    ctx->rec_packed = gs::rec_packed(P);
+    for (int c = 0; c < 3; ++c)
+        P.campos[c] = -(u->view[4 * c + 0] * u->view[12] + u->view[4 * c + 1] * u->view[13] +
+                        u->view[4 * c + 2] * u->view[14]);
+    Lane &L = *ctx->L;
+    uint64_t *cur = L.lb + (size_t)L.lb_par * L.lb_cap, *nxt = L.lb + (size_t)(L.lb_par ^ 1) * L.lb_cap;
+    gs::LookbackDev lb{cur, nxt, L.lb_cap};
+    L.lb_par ^= 1;
+    gs::launch_pre_emit(L.stream, P, scene_dev(scene), frame_dev(ctx), lb, lazy_loads(ctx, n), L.keys, L.vals, (uint32_t)L.e_cap,
+                        prefix_hist, fev(ctx, 0), fev(ctx, 1));
+    GS_HIP(ctx, hipGetLastError());
+    ctx->n = n;
+    L.split = true;
+    L.keys_sorted = true;
+    L.vals_partial = false;
+    L.pe_scene = scene;
+    L.pe_P = P;
     return GS_OK;
 }
 
@@ -855,11 +963,13 @@ int enqueue_emit(gs_ctx *ctx, uint32_t *prefix_hist = nullptr) {
 // the bins stage is then empty (its timing event follows the sort's)
 // A frame sort with bins leaves the keys unsorted (the blend reads the values and the bins
 // only) when the splat ids fit 24 bits; gs_frame_read(GS_READ_KEYS) then sorts again.
+// small: the small-frame form (with bins, no prefix; keys come out sorted)
 int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false,
-                 const gs::PrefixDev *pre = nullptr) {
-    const bool keys_out = !pre && (!with_bins || ctx->n > (1 << 24));
+                 const gs::PrefixDev *pre = nullptr, int64_t dup_base = -1, bool small = false) {
+    small = small && with_bins && !pre;
+    const bool keys_out = small || (!pre && (!with_bins || ctx->n > (1 << 24)));
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre))
+                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre, dup_base, small))
         return set_error(ctx, rc, ctx->err);
     ctx->L->keys_sorted = keys_out;
     ctx->L->vals_partial = pre != nullptr;
@@ -907,8 +1017,15 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
         mw = std::max(mw, P.xb[t + 1] - P.xb[t]);
         mh = std::max(mh, P.yb[t + 1] - P.yb[t]);
     }
-    P.nbx = (mw + 15) / 16;
-    P.nby = (mh + 15) / 16;
+    // the sub-block form: the spec frame's count is the newest one seen (this frame's is on the device)
+    const int64_t e_est = count ? ctx->E : E;
+    const int64_t sub16 = (int64_t)gs::kTiles * gs::kTiles * ((mw + 15) / 16) * ((mh + 15) / 16);
+    const bool small = ctx->draw_sub == 8 || (ctx->draw_sub == 0 && e_est < ctx->small_draw_entries &&
+                                              sub16 <= kSmallDrawSubBlocks);
+    const int sb = small ? 8 : 16;
+    ctx->last_draw_sub = sb;
+    P.nbx = (mw + sb - 1) / sb;
+    P.nby = (mh + sb - 1) / sb;
     const size_t npx = (size_t)width * height;
     uint32_t *dst = (uint32_t *)out_rgba8;
     if (!out_on_device) {
@@ -936,7 +1053,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
         if (sl.draw_out == dst || (with_stats && sl.draw_stats))
             GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->ev[i][kEv - 1], 0));
     }
-    gs::launch_draw(ctx->L->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, ctx->L->bins, ctx->L->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
+    gs::launch_draw(ctx->L->stream, P, (flags & GS_FLAG_FAST_EXP) != 0, small, ctx->L->bins, ctx->L->vals, frame_dev(ctx), colour, dst, (flags & GS_FLAG_DRAW_STATS) ? ctx->draw_stats : nullptr, fev(ctx, 7),
                     fev(ctx, 8));
     GS_HIP(ctx, hipGetLastError());
     gs_ctx::Slot &me = ctx->slot[ctx->cur];
@@ -956,7 +1073,8 @@ int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
                 int out_on_device, gs_frame_stats *stats) {
     int rc;
     if ((rc = gs_preprocess(ctx, scene, u, flags, stats))) return rc;
-    if ((rc = enqueue_sort(ctx, ctx->E, nullptr, true))) return rc;  // gs_sort + gs_compute_bins
+    if ((rc = enqueue_sort(ctx, ctx->E, nullptr, true, nullptr, -1, ctx->E < ctx->small_sort_entries)))
+        return rc;  // gs_sort + gs_compute_bins
     ctx->stage = 3;
     // src/Splats.cpp:596 draw(width, height, float(width) / 16.f, float(height) / 16.f)
     return gs_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags, out,
@@ -969,18 +1087,12 @@ int render_sync(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
 int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags, void *out) {
     if (int rc = prepare_frame(ctx)) return rc;
     if (int rc = next_lane(ctx)) return rc;
-    const int64_t want = std::max<int64_t>(ctx->E + ctx->E / 4 + 65536, (int64_t)scene->n + 4096);
+    // (the split layout of the fused kernel, small scenes, holds the duplicates from index n on:
+    // n + D entries)
+    const int64_t n = scene->n;
+    const int64_t want = std::max<int64_t>(ctx->E + ctx->E / 4 + 65536, n + ctx->D + ctx->D / 4 + 65536);
     if (ctx->L->e_cap < want)
         if (int rc = ensure_entries(ctx, want)) return rc;
-    if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
-    gs_ctx::Slot &sl = ctx->slot[ctx->cur];
-    sl.spec = true;
-    sl.scene = scene;
-    sl.u = *u;
-    sl.flags = flags;
-    sl.out = out;
-    sl.cap = ctx->L->e_cap;
-    const uint32_t *cnt = ctx->L->totals;
     // prefix sort: frames of the size where the lists are long (the last observed count)
     const bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_target;
     gs::PrefixDev pd{};
@@ -989,7 +1101,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
             GS_HIP(ctx, hipMalloc(&ctx->L->pre_buf, gs::kPrefixWords * 4));
             GS_HIP(ctx, hipMemsetAsync(ctx->L->pre_buf, 0, gs::kPrefixWords * 4, ctx->L->stream));
         }
-        uint32_t *b = ctx->L->pre_buf;
+        uint32_t *b = ctx->L->pre_buf;  // (the lane's: enqueue_pre_emit keeps the lane)
         pd.hist = b;
         pd.theta = pd.hist + (size_t)gs::kPrefixHistCopies * 256 * gs::kPrefixBuckets;
         pd.counts = pd.theta + gs::kClasses;
@@ -999,19 +1111,44 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         // passes 1-3 sized for the kept count of the newest retired prefix-sorted frame + 25 %
         // (+ 64Ki); the first one: every entry
         const int64_t cap_e = ctx->L->e_cap;
-        pd.cap_sel = (uint32_t)(ctx->prefix_kept ? std::min<int64_t>(cap_e, (int64_t)ctx->prefix_kept * 5 / 4 + 65536)
-                                                 : cap_e);
-        sl.cap_sel = pd.cap_sel;
-        pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
+        // (scaled by the depth since: a miss doubles it, and the kept count roughly with it)
+        const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
+                                 ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
+                                 : (int64_t)ctx->prefix_kept;
+        pd.cap_sel = (uint32_t)(ctx->prefix_kept ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536) : cap_e);
         pd.target = (uint32_t)ctx->prefix_target;
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
+    }
+    const bool fused = gs::preprocess_blocks(scene->n) <= kFusedMaxBlocks;
+    if (fused) {
+        if (int rc = enqueue_pre_emit(ctx, scene, u, flags, prefix ? pd.hist : nullptr)) return rc;
+    } else {
+        if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
+    }
+    gs_ctx::Slot &sl = ctx->slot[ctx->cur];
+    sl.spec = true;
+    sl.scene = scene;
+    sl.u = *u;
+    sl.flags = flags;
+    sl.out = out;
+    sl.cap = ctx->L->e_cap;
+    sl.fused = fused;
+    sl.n = scene->n;
+    const uint32_t *cnt = ctx->L->totals;
+    if (prefix) {
+        sl.cap_sel = pd.cap_sel;
+        sl.target = ctx->prefix_target;
+        pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
         sl.prefix = true;
         ctx->prefix_frames += 1;
     }
     int rc;
-    if ((rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr)) ||
-        (rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr)))
+    // the emission (the fused kernel's is done); the sort sized by the capacity (the entry count
+    // stays on the device), reading the fused kernel's split layout as V + D entries
+    if (!fused && (rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr))) return rc;
+    if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
+                           ctx->E < ctx->small_sort_entries)))
         return rc;
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
                            out, 1, ctx->L->e_cap, cnt, prefix)))
@@ -1066,8 +1203,10 @@ int gs_compute_bins(gs_ctx *ctx) {
     if (int rc = validate_all(ctx)) return rc;
     if (ctx->stage < 2) return set_error(ctx, GS_ERR_STATE, "gs_compute_bins: call gs_sort first");
     if (int rc = use_device(ctx)) return rc;
-    if (ctx->L->vals_partial)
-        if (int rc = resort_full(ctx)) return rc;  // (a prefix sort left the keys buffer as scratch)
+    // the bins count the sorted keys: after a frame sort that left only the values sorted (or only
+    // each list's prefix), the frame's entries are sorted again with their keys
+    if (!ctx->L->keys_sorted || ctx->L->vals_partial)
+        if (int rc = resort_full(ctx)) return rc;
     if (int rc = enqueue_bins(ctx, ctx->E, nullptr)) return rc;
     ctx->stage = 3;
     return GS_OK;
@@ -1150,7 +1289,15 @@ namespace {
 // that left the keys unsorted (keys_sorted false) or sorted only each list's prefix
 // (vals_partial), for the stage calls and readbacks that need the whole sorted pairs.
 int resort_full(gs_ctx *ctx) {
-    if (ctx->stage < 2 || (ctx->L->keys_sorted && !ctx->L->vals_partial)) return GS_OK;
+    if (ctx->stage < 2 || (ctx->L->keys_sorted && !ctx->L->vals_partial && !ctx->L->split)) return GS_OK;
+    if (ctx->L->split) {  // a fused frame wrote no emission records: preprocess it again (staged path)
+        if (!ctx->L->pe_scene) return set_error(ctx, GS_ERR_STATE, "the frame's scene was destroyed");
+        const gs::FrameDev fr = frame_dev(ctx);
+        gs::launch_preprocess(ctx->L->stream, ctx->L->pe_P, scene_dev(ctx->L->pe_scene), fr, nullptr);
+        gs::launch_scan_blocksums(ctx->L->stream, fr, gs::preprocess_blocks(ctx->L->pe_P.n), nullptr, nullptr);
+        GS_HIP(ctx, hipGetLastError());
+        ctx->L->split = false;
+    }
     gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals,
                     (uint32_t)ctx->L->e_cap, nullptr, nullptr);
     GS_HIP(ctx, hipGetLastError());
@@ -1166,8 +1313,27 @@ extern "C" {
 
 int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
-    if (target >= 0) ctx->prefix_target = target;
+    if (target >= 0) {
+        ctx->prefix_base = ctx->prefix_target = target;
+        ctx->prefix_clean_run = 0;
+    }
     if (current) *current = ctx->prefix_target;
+    return GS_OK;
+}
+
+int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entries) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (draw_entries >= 0) ctx->small_draw_entries = draw_entries;
+    if (sort_entries >= 0) ctx->small_sort_entries = sort_entries;
+    return GS_OK;
+}
+
+int gs_ctx_set_draw_sub(gs_ctx *ctx, int sub, int *current) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (sub != -1 && sub != 0 && sub != 8 && sub != 16)
+        return set_error(ctx, GS_ERR_INVALID, "gs_ctx_set_draw_sub: sub must be 0 (by entry count), 8 or 16");
+    if (sub >= 0) ctx->draw_sub = sub;
+    if (current) *current = ctx->last_draw_sub;
     return GS_OK;
 }
 
@@ -1215,6 +1381,17 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         if (ctx->stage < 3) return set_error(ctx, GS_ERR_STATE, "gs_frame_read: bins not computed");
         src = ctx->L->bins; avail = 256; break;
     case GS_READ_MEANS2D:
+    case GS_READ_CONICS:
+    case GS_READ_CULLBOX:
+        // a fused frame (k_pre_emit) wrote no emission records, which mark the culled rows:
+        // preprocess it again on the staged path (same records, and the emission records)
+        if (ctx->L->split)
+            if (int rc = resort_full(ctx)) return rc;
+        break;
+    default: break;
+    }
+    switch (what) {
+    case GS_READ_MEANS2D:
     case GS_READ_CONICS: {  // fields of the 32-byte blend records
         const size_t comps = what == GS_READ_MEANS2D ? 2 : 4, off = what == GS_READ_MEANS2D ? 0 : 8;
         if (count > comps * (size_t)ctx->n) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");
@@ -1259,6 +1436,9 @@ int gs_frame_read(gs_ctx *ctx, int what, void *host_dst, size_t count) {
         }
         return GS_OK;
     }
+    case GS_READ_KEYS:
+    case GS_READ_VALS:
+    case GS_READ_BINS: break;
     default: return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: unknown buffer");
     }
     if (count > avail) return set_error(ctx, GS_ERR_INVALID, "gs_frame_read: count exceeds the buffer");

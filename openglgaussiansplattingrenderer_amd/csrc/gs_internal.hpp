@@ -136,7 +136,7 @@ struct DrawParams {
     const uint32_t *count;      // device (V, D): E = min(E, V + D), or null
     int32_t clean;
     int32_t no_cull;
-    int32_t nbx, nby;           // max 16x16 sub-blocks per coarse tile in x / y
+    int32_t nbx, nby;           // max sub-blocks (16x16, or 8x8 in the small form) per coarse tile in x / y
     int32_t coverW, coverH;     // drawn coverage; pixels outside it are zeroed (Q9)
     int32_t n;                  // splats of the scene
     int32_t V;                  // splats with entries (when count is null; else count[0])
@@ -165,10 +165,16 @@ struct SortScratch {
 // an intermediate order.
 // pre != null (with bins and dev_count): the frame's prefix sort (see PrefixDev): vals holds
 // the sorted values at the positions bins[kBinsLimit + t] marks as sorted, keys are not output.
+// dup_base >= 0 (with dev_count): the input is k_pre_emit's split layout, V = dev_count[0] mains
+// at [0, V) and the dev_count[1] duplicates at [dup_base, dup_base + D); the first pass reads it
+// as one array of V + D entries (n is then the capacity of that virtual array).
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
-               uint32_t *bins = nullptr, bool keys_out = true, const PrefixDev *pre = nullptr);
-int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s);
+               uint32_t *bins = nullptr, bool keys_out = true, const PrefixDev *pre = nullptr,
+               int64_t dup_base = -1, bool small = false);
+// small (not with pre): the form for few entries -- 8 launches instead of 12 (k_sweep_small);
+// keys and values come out sorted.  Any n is sorted correctly; it pays off while n is small.
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small = false);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]
 void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, uint32_t *kout, int64_t n,
@@ -209,12 +215,28 @@ struct FrameDev {
 };
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
 // start / stop: optional hipEvents recorded on the dispatch packets (stage timing)
-void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start);
+// lazy: the covariance / opacity loads only for the splats inside the NDC square (preprocess_one)
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
+                       bool lazy = false);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);
 bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preprocess) fits this frame
 // prefix_hist != null: also sample the emitted keys into the prefix sort's histogram
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
                  hipEvent_t start, hipEvent_t stop, uint32_t *prefix_hist = nullptr);
+// The fused preprocess + emission of a frame enqueued without a host round trip (k_pre_emit):
+// its decoupled look-back state, two halves per frame lane used by alternate frames (each frame
+// clears the other half for the next one).
+struct LookbackDev {
+    uint64_t *st;          // [cap_blocks] this frame's per-workgroup status words (zero on entry)
+    uint64_t *st_next;     // the other half, cleared by this frame
+    uint32_t cap_blocks;
+};
+// mains at [0, V), duplicates at [n, n + D) of keys / vals (the sort's first pass reads them as
+// one array, sort_pairs' dup_base); (V, D) into fr.totals and the frame's pinned ring slot.
+// lazy: the covariance / opacity loads only for the splats inside the NDC square.
+void launch_pre_emit(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const LookbackDev &lb,
+                     bool lazy, uint32_t *keys, uint32_t *vals, uint32_t cap, uint32_t *prefix_hist, hipEvent_t start,
+                     hipEvent_t stop);
 // E entries, or min(E, dev_count[0] + dev_count[1]) when dev_count is given; counts must be
 // zero on entry and are left zero
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,
@@ -234,8 +256,9 @@ constexpr int kDrawTraceBlocks = 65536;
 constexpr int kDrawTraceWords = 16;
 constexpr size_t kDrawStatsBytes = (size_t)kDrawTraceBlocks * kDrawTraceWords * 4;
 
-void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats, hipEvent_t start,
-                 hipEvent_t stop);
+// small: the 8x8 one-pixel-per-lane form (P.nbx / P.nby then count 8-pixel sub-blocks)
+void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, bool small, const uint32_t *bins,
+                 const uint32_t *vals, const FrameDev &fr, const float4 *colour, uint32_t *out,
+                 unsigned long long *stats, hipEvent_t start, hipEvent_t stop);
 
 }  // namespace gs

@@ -184,127 +184,135 @@ __device__ __forceinline__ uint2 pack_box(const float4 &b) {
     return make_uint2(lo(b.x) | (hi(b.y) << 16), lo(b.z) | (hi(b.w) << 16));
 }
 
+// One splat of preprocess.glsl:64-190: its blend record, cull box and (GS_FLAG_SH) colour
+// written when it has entries, and its emission record returned: (z01 bits, tileX, tileY, rect)
+// or (0, -1, -1, 0) without entries (culled, det == 0, or i out of range).
 // CLEAN: clean mode (P.clean) as a template parameter -- a uniform flag's alternatives were
-// if-converted into selects that every splat evaluated
-template <bool PACK, bool CLEAN>
-__global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
-    __shared__ uint32_t s_wave[kBlock / 64];
-    uint32_t n_main = 0, n_dup = 0;
-#pragma unroll 1
-    for (int it = 0; it < kPer; ++it) {
-    const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
-    if (i < P.n) {
-        // all ten planes in one round trip (the covariance and opacity of culled splats are
-        // read for nothing: 28 B of 40 for 24 % of C3's splats, cheaper than a second trip)
-        const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
-        const size_t n = (size_t)P.n;
-        const float c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
-        const float c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
-        const float opac = sc.opacity[i];
-        // Straight-line body: every cull folds into `vis` and the outputs are selected at the
-        // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
-        // all ten plane loads issue up front and no exec-mask bookkeeping runs).  Culled lanes
-        // compute garbage (inf / NaN) that is never used.
-        // :77-78
-        float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
-        float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
-        float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
-        const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
-        const float w = fmaxf(p3, 0.0001f);
-        p0 = p0 / w;
-        p1 = p1 / w;
-        p2 = p2 / w;
-        // :80-89 cull: NDC x/y only
-        bool vis = !(p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f);
-        // :91-94
-        float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
-        const float sz = (p2 + 1.0f) * 0.5f;
-        sx = sx * (float)P.W;
-        sy = sy * (float)P.H;
-        if (CLEAN) vis = vis && (sz >= 0.0f && sz <= 1.0f);  // clean: near/far cull (Q6)
-        // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
-        const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
-        const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
-                        {P.view[8], P.view[9], P.view[10]}}};
-        // :110-116
-        float tx = m4v_row(P.view, 0, mx, my, mz, 1.0f);
-        float ty = m4v_row(P.view, 1, mx, my, mz, 1.0f);
-        const float tz = m4v_row(P.view, 2, mx, my, mz, 1.0f);
-        const float limx = -1.3f * P.tan_fov_x, limy = -1.3f * P.tan_fov_y;
-        const float txtz = tx / tz, tytz = ty / tz;
-        tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
-        ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
-        // :118-128
-        const M3 J = {{{P.fx / tz, 0.0f, -(P.fx * tx) / (tz * tz)},
-                       {0.0f, P.fy / tz, -(P.fy * ty) / (tz * tz)},
-                       {0.0f, 0.0f, 0.0f}}};
-        const M3 T = mul3(tr3(W3), J);
-        M3 C = mul3(mul3(tr3(T), tr3(Sig)), T);
-        C.v[0][0] += 0.3f;
-        C.v[1][1] += 0.3f;
-        // :129-136
-        const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
-        const float det = ca * cc - cb * cb;
-        vis = vis && det != 0;  // Q7: entry omitted
-        if (CLEAN) vis = vis && det > 0.0f;
-        const float inv = 1.0f / det;
-        const float4 cov2 = make_float4(cc * inv, -cb * inv, ca * inv, opac);
-        // :139-149
-        const float middle = (cc + ca) * 0.5f;
-        const float l1 = middle + sqrtf(fmaxf(0.1f, middle * middle - det));
-        const float l2 = middle - sqrtf(fmaxf(0.1f, middle * middle - det));
-        const float radius = ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
-        const int minX = max(0, f2i((sx - radius) / P.tile_w));
-        const int maxX = min(15, f2i((sx + radius) / P.tile_w));
-        const int minY = max(0, f2i((sy - radius) / P.tile_h));
-        const int maxY = min(15, f2i((sy + radius) / P.tile_h));
-        // :151-155 main tile (unclamped in ref mode, Q5)
-        int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
-        if (CLEAN) {
-            tileX = min(15, max(0, tileX));
-            tileY = min(15, max(0, tileY));
+// if-converted into selects that every splat evaluated.
+// LAZY: the covariance and opacity (28 of the 40 bytes) are loaded only for the lanes that pass
+// the NDC cull, one round trip later -- for frames where most splats are culled (the small C5
+// views: ~97 % culled, a 64-byte line of a plane then mostly holds culled splats only);
+// otherwise all ten planes are loaded in one round trip.
+template <bool CLEAN, bool LAZY>
+__device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDev &sc, const FrameDev &fr, int i,
+                                               bool valid) {
+    if (!valid) return make_int4(0, -1, -1, 0);
+    const size_t n = (size_t)P.n;
+    const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
+    float c0, c1, c2, c3, c4, c5, opac;
+    if (!LAZY) {  // all ten planes in one round trip (see LAZY)
+        c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
+        c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
+        opac = sc.opacity[i];
+    }
+    // Straight-line body: every cull folds into `vis` and the outputs are selected at the
+    // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
+    // all ten plane loads issue up front and no exec-mask bookkeeping runs).  Culled lanes
+    // compute garbage (inf / NaN) that is never used.
+    // :77-78
+    float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
+    float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
+    float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
+    const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
+    const float w = fmaxf(p3, 0.0001f);
+    p0 = p0 / w;
+    p1 = p1 / w;
+    p2 = p2 / w;
+    // :80-89 cull: NDC x/y only
+    bool vis = !(p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f);
+    if (LAZY) {
+        c0 = c1 = c2 = c3 = c4 = c5 = opac = 0.0f;
+        if (vis) {
+            c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
+            c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
+            opac = sc.opacity[i];
         }
-        const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
-        const int mainInRect = (tileX >= minX && tileX <= maxX && tileY >= minY && tileY <= maxY) ? 1 : 0;
-        n_main += vis ? 1u : 0u;
-        n_dup += vis ? (uint32_t)(rectCount - mainInRect) : 0u;
-        const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
-                            ((uint32_t)maxY << 24);
+    }
+    // :91-94
+    float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
+    const float sz = (p2 + 1.0f) * 0.5f;
+    sx = sx * (float)P.W;
+    sy = sy * (float)P.H;
+    if (CLEAN) vis = vis && (sz >= 0.0f && sz <= 1.0f);  // clean: near/far cull (Q6)
+    // :98-108 covariance (symmetric) and W3 (upper-left of the view matrix)
+    const M3 Sig = {{{c0, c1, c2}, {c1, c3, c4}, {c2, c4, c5}}};
+    const M3 W3 = {{{P.view[0], P.view[1], P.view[2]}, {P.view[4], P.view[5], P.view[6]},
+                    {P.view[8], P.view[9], P.view[10]}}};
+    // :110-116
+    float tx = m4v_row(P.view, 0, mx, my, mz, 1.0f);
+    float ty = m4v_row(P.view, 1, mx, my, mz, 1.0f);
+    const float tz = m4v_row(P.view, 2, mx, my, mz, 1.0f);
+    const float limx = -1.3f * P.tan_fov_x, limy = -1.3f * P.tan_fov_y;
+    const float txtz = tx / tz, tytz = ty / tz;
+    tx = fminf(limx, fmaxf(-limx, txtz)) * tz;
+    ty = fminf(limy, fmaxf(-limy, tytz)) * tz;
+    // :118-128
+    const M3 J = {{{P.fx / tz, 0.0f, -(P.fx * tx) / (tz * tz)},
+                   {0.0f, P.fy / tz, -(P.fy * ty) / (tz * tz)},
+                   {0.0f, 0.0f, 0.0f}}};
+    const M3 T = mul3(tr3(W3), J);
+    M3 C = mul3(mul3(tr3(T), tr3(Sig)), T);
+    C.v[0][0] += 0.3f;
+    C.v[1][1] += 0.3f;
+    // :129-136
+    const float ca = C.v[0][0], cb = C.v[0][1], cc = C.v[1][1];
+    const float det = ca * cc - cb * cb;
+    vis = vis && det != 0;  // Q7: entry omitted
+    if (CLEAN) vis = vis && det > 0.0f;
+    const float inv = 1.0f / det;
+    const float4 cov2 = make_float4(cc * inv, -cb * inv, ca * inv, opac);
+    // :139-149
+    const float middle = (cc + ca) * 0.5f;
+    const float l1 = middle + sqrtf(fmaxf(0.1f, middle * middle - det));
+    const float l2 = middle - sqrtf(fmaxf(0.1f, middle * middle - det));
+    const float radius = ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+    const int minX = max(0, f2i((sx - radius) / P.tile_w));
+    const int maxX = min(15, f2i((sx + radius) / P.tile_w));
+    const int minY = max(0, f2i((sy - radius) / P.tile_h));
+    const int maxY = min(15, f2i((sy + radius) / P.tile_h));
+    // :151-155 main tile (unclamped in ref mode, Q5)
+    int tileX = f2i(sx / P.tile_w), tileY = f2i(sy / P.tile_h);
+    if (CLEAN) {
+        tileX = min(15, max(0, tileX));
+        tileY = min(15, max(0, tileY));
+    }
+    const uint32_t rp = (uint32_t)min(minX, 16) | ((uint32_t)maxX << 8) | ((uint32_t)min(minY, 16) << 16) |
+                        ((uint32_t)maxY << 24);
 
-        // Conservative pixel box of the region where alpha >= 1/255 can hold
-        // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
-        // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
-        // culling an entry outside the box never changes a pixel.
-        // The box and the pre-exp threshold only cull (they never enter a pixel's
-        // arithmetic) and carry margins far above hardware-instruction error (0.05 in ln,
-        // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
-        // v_sqrt instead of the correctly rounded library sequences.
-        const float A = cov2.x, B = cov2.y, Cq = cov2.z;
-        const float lg = draw_log255o(opac);  // ln(255 o)
-        const float tau = lg + 0.05f;
-        const float detQ = A * Cq - B * B;
-        const float trq = A + Cq;
-        const bool wellc = A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ;
-        const float rq = __builtin_amdgcn_rcpf(detQ);
-        const float hx = __builtin_amdgcn_sqrtf(2.0f * tau * Cq * rq) * 1.02f + 1.0f;
-        const float hy = __builtin_amdgcn_sqrtf(2.0f * tau * A * rq) * 1.02f + 1.0f;
-        const float inf = __builtin_inff();
-        // tau <= 0: never reaches 1/255 anywhere (empty box); ill-conditioned: unbounded box
-        const float4 box = !(tau > 0.0f) ? make_float4(inf, -inf, inf, -inf)
-                           : wellc       ? make_float4(sx - hx, sx + hx, sy - hy, sy + hy)
-                                         : make_float4(-inf, inf, -inf, inf);
-        const float2 m2 = make_float2(sx, sy);
-        const float4 co = cov2;
-        const int4 rc = vis ? make_int4((int)f2u(sz), tileX, tileY, (int)rp) : make_int4(0, -1, -1, 0);
-        // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
-        // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
-        // becomes -inf, which never skips
-        // the blend record, box and (GS_FLAG_SH) colour are read only through entries: written
-        // for the splats that have some (gs_frame_read shows the others as culled), and for
-        // splat 0, which the reference's culled entries draw (preprocess.glsl:80-88 splatKeys = 0,
-        // reached by a Q10 over-read; k_draw): without entries its record is the culled one --
-        // means2D, conic and opacity 0 (never blends: threshold +inf, empty box)
-        if (rc.y >= 0) {
+    // Conservative pixel box of the region where alpha >= 1/255 can hold
+    // (draw.glsl:115-126): q = A dx^2 + 2B dx dy + C dy^2 <= 2 ln(255 o).  Margins
+    // cover the rounding of power/exp (relative q error <= ~6 eps * cond), so
+    // culling an entry outside the box never changes a pixel.
+    // The box and the pre-exp threshold only cull (they never enter a pixel's
+    // arithmetic) and carry margins far above hardware-instruction error (0.05 in ln,
+    // 2 % in the half-widths, 1e-3 in the threshold), so they use v_log / v_rcp /
+    // v_sqrt instead of the correctly rounded library sequences.
+    const float A = cov2.x, B = cov2.y, Cq = cov2.z;
+    const float lg = draw_log255o(opac);  // ln(255 o)
+    const float tau = lg + 0.05f;
+    const float detQ = A * Cq - B * B;
+    const float trq = A + Cq;
+    const bool wellc = A > 0.0f && Cq > 0.0f && detQ > 0.0f && trq * trq < 1.0e5f * detQ;
+    const float rq = __builtin_amdgcn_rcpf(detQ);
+    const float hx = __builtin_amdgcn_sqrtf(2.0f * tau * Cq * rq) * 1.02f + 1.0f;
+    const float hy = __builtin_amdgcn_sqrtf(2.0f * tau * A * rq) * 1.02f + 1.0f;
+    const float inf = __builtin_inff();
+    // tau <= 0: never reaches 1/255 anywhere (empty box); ill-conditioned: unbounded box
+    const float4 box = !(tau > 0.0f) ? make_float4(inf, -inf, inf, -inf)
+                       : wellc       ? make_float4(sx - hx, sx + hx, sy - hy, sy + hy)
+                                     : make_float4(-inf, inf, -inf, inf);
+    const float2 m2 = make_float2(sx, sy);
+    const float4 co = cov2;
+    const int4 rc = vis ? make_int4((int)f2u(sz), tileX, tileY, (int)rp) : make_int4(0, -1, -1, 0);
+    // pre-exp threshold of the blend: power < thr implies alpha < 1/255 (draw.glsl:123-126)
+    // for any exp within a few ulp; 255*o <= 0 gives +inf (never blends); NaN (opacity NaN)
+    // becomes -inf, which never skips
+    // the blend record, box and (GS_FLAG_SH) colour are read only through entries: written
+    // for the splats that have some (gs_frame_read shows the others as culled), and for
+    // splat 0, which the reference's culled entries draw (preprocess.glsl:80-88 splatKeys = 0,
+    // reached by a Q10 over-read; k_draw): without entries its record is the culled one --
+    // means2D, conic and opacity 0 (never blends: threshold +inf, empty box)
+    if (rc.y >= 0) {
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w};
         fr.cullbox[i] = pack_box(box);
         if (P.sh) {  // GS_FLAG_SH: this frame's colour
@@ -313,21 +321,41 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
             dx = dx / len;
             dy = dy / len;
             dz = dz / len;
-            const size_t n = (size_t)P.n;
             fr.col[i] = make_float4(sh_channel(sc.sh, n, i, 0, dx, dy, dz), sh_channel(sc.sh, n, i, 1, dx, dy, dz),
                                     sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
         }
-        }
-        else if (i == 0) {  // splat 0 culled: the record its culled entries draw
-            fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // threshold +inf
-            fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
-        }
-        if (PACK)
-            reinterpret_cast<uint2 *>(fr.rec)[i] =
-                make_uint2((uint32_t)rc.x, rc.y >= 0 ? pack_rec(rc.y, rc.z, (uint32_t)rc.w) : 0u);
-        else
-            fr.rec[i] = rc;
+    } else if (i == 0) {  // splat 0 culled: the record its culled entries draw
+        fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // threshold +inf
+        fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
     }
+    return rc;
+}
+
+// duplicates of an emission record: the rect's tiles minus the main tile when it lies in the rect
+__device__ __forceinline__ uint32_t rec_dups(const int4 &rc) {
+    const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
+    const int rectCount = (maxX >= minX && maxY >= minY) ? (maxX - minX + 1) * (maxY - minY + 1) : 0;
+    const int mainInRect = (rc.y >= minX && rc.y <= maxX && rc.z >= minY && rc.z <= maxY) ? 1 : 0;
+    return rc.y >= 0 ? (uint32_t)(rectCount - mainInRect) : 0u;
+}
+
+template <bool PACK, bool CLEAN, bool LAZY>
+__global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
+    __shared__ uint32_t s_wave[kBlock / 64];
+    uint32_t n_main = 0, n_dup = 0;
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+        const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
+        const int4 rc = preprocess_one<CLEAN, LAZY>(P, sc, fr, i, i < P.n);
+        n_main += rc.y >= 0 ? 1u : 0u;
+        n_dup += rec_dups(rc);
+        if (i < P.n) {
+            if (PACK)
+                reinterpret_cast<uint2 *>(fr.rec)[i] =
+                    make_uint2((uint32_t)rc.x, rc.y >= 0 ? pack_rec(rc.y, rc.z, (uint32_t)rc.w) : 0u);
+            else
+                fr.rec[i] = rc;
+        }
     }
     // block sums of (main, dup) for the emission offsets
     uint32_t tot_main, tot_dup;
@@ -560,9 +588,12 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
         const uint32_t r0[2] = {off.x, V + off.y}, r1[2] = {carry_m, V + carry_d};
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-            const uint32_t j = (r0[r] + kPrefixSample - 1) / kPrefixSample + threadIdx.x;
-            const uint32_t p = j * kPrefixSample;
-            if (p < r1[r] && p < cap) {
+            // every sample position of the range (a workgroup's duplicate range can hold up to
+            // 256 splats x 256 tiles = 65536 entries, more than one sample per thread covers)
+            const uint32_t lim = min(r1[r], cap);
+            for (uint32_t j = (r0[r] + kPrefixSample - 1) / kPrefixSample + threadIdx.x; j * kPrefixSample < lim;
+                 j += kBlock) {
+                const uint32_t p = j * kPrefixSample;
                 const uint32_t key = keys[p];
                 const uint32_t c = key_class(key);
                 if (c < 256u)
@@ -571,6 +602,209 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
                               1u);
             }
         }
+    }
+}
+
+// ------------------------------------------------ fused preprocess + emission (frame path)
+// k_pre_emit: one pass over the splats for a frame enqueued without a host round trip.  Each
+// workgroup preprocesses its 1024 splats (wave w: splats [256 w, 256 w + 256) as four items of
+// 64), keeps their emission records in registers, learns its entry offsets by a decoupled
+// look-back over the workgroups before it (single-pass scan: a workgroup publishes its (main,
+// dup) counts, then their inclusive prefix), and emits its entries.  This removes the 8-byte
+// emission record written and read back (98 MB per C3 frame), the block-sum scan launch and the
+// separate emission pass of k_preprocess -> k_scan_blocksums -> k_emit.
+// Entry layout ("split"): mains at [0, V) in splat order as before, duplicates at [dup_base,
+// dup_base + D) splat-major -- a workgroup cannot know V (the mains of the workgroups after it)
+// when it emits, so the duplicates start at dup_base = n >= V.  The sort's first pass reads the
+// two ranges as one array of V + D entries (the same order as the contiguous layout), so the
+// sorted result is unchanged.
+// Forward progress: a workgroup waits only on workgroups with lower ids, which publish their
+// counts right after their own preprocessing.  The hardware dispatches a grid in id order (per
+// XCD, round-robin over them), so they are running or done; HIP does not promise that order
+// (MI355X_MICROARCH.md, "Workgroup dispatch"), so a wait is bounded: after kLbSpinLimit polls
+// (~tens of ms) it gives up, the workgroup goes on with what it has (every store stays inside the
+// entry capacity) and flags the frame (ring word 2), which the host renders again on the
+// host-synchronous path.  Nothing depends on the order for correctness.  (A ticket counter
+// instead of the workgroup id serialised every workgroup's start on one address: ~33 ns each,
+// 0.2 ms for the 6000 workgroups of C3.)
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
+constexpr uint32_t kLbSpinLimit = 1u << 15;
+__device__ __forceinline__ uint64_t lb_word(uint64_t flag, uint32_t m, uint32_t d) {
+    return flag | ((uint64_t)(d & 0x7fffffffu) << 31) | (uint64_t)(m & 0x7fffffffu);
+}
+__device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool PACK, bool CLEAN, bool LAZY>
+__global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, FrameDev fr, LookbackDev lb,
+                                                     uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                                                     uint32_t cap, uint32_t dup_base, uint32_t *__restrict__ phist,
+                                                     uint32_t nblocks) {
+    // the workgroup's emission records and per-item inclusive duplicate counts stay in LDS between
+    // the preprocessing and the emission (in registers they held the kernel to 5 waves per SIMD)
+    using Rec = typename std::conditional<PACK, uint2, int4>::type;
+    __shared__ Rec s_rec[kSplatsPerBlock];
+    __shared__ uint16_t s_incl[kBlock / 64][kPer][64];  // (<= 64 * 256 per item)
+    __shared__ uint2 s_tot[kBlock / 64];
+    __shared__ uint2 s_off;
+    const uint32_t blk = blockIdx.x;
+    // the next frame of this lane uses the other half: clear it (its previous user, this lane's
+    // frame before, is complete)
+    for (uint32_t j = blk * kBlock + threadIdx.x; j < lb.cap_blocks; j += nblocks * kBlock) lb.st_next[j] = 0ull;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const int wbase = (int)blk * kSplatsPerBlock + wid * (kPer * 64);
+    Rec *wrec = s_rec + wid * (kPer * 64);
+    uint32_t tot_m = 0, tot_d = 0;
+#pragma unroll 1
+    for (int j = 0; j < kPer; ++j) {
+        const int i = wbase + j * 64 + lane;
+        const int4 rc = preprocess_one<CLEAN, LAZY>(P, sc, fr, i, i < P.n);
+        if constexpr (PACK)
+            wrec[j * 64 + lane] = make_uint2((uint32_t)rc.x, rc.y >= 0 ? pack_rec(rc.y, rc.z, (uint32_t)rc.w) : 0u);
+        else
+            wrec[j * 64 + lane] = rc;
+        const uint32_t incl = wave_incl_scan(rec_dups(rc));
+        s_incl[wid][j][lane] = (uint16_t)incl;
+        tot_m += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(rc.y >= 0));
+        tot_d += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    if (lane == 0) s_tot[wid] = make_uint2(tot_m, tot_d);
+    __syncthreads();
+    uint32_t wm = 0, wd = 0, all_m = 0, all_d = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint2 t = s_tot[w];
+        wm += w < wid ? t.x : 0u;
+        wd += w < wid ? t.y : 0u;
+        all_m += t.x;
+        all_d += t.y;
+    }
+    if (wid == 0) {  // the look-back (one wave): this workgroup's exclusive (mains, dups) offsets
+        uint32_t exm = 0, exd = 0;
+        bool fail = false;
+        if (blk == 0) {
+            if (lane == 0) lb_store(&lb.st[0], lb_word(kLbInc, all_m, all_d));
+        } else {
+            if (lane == 0) lb_store(&lb.st[blk], lb_word(kLbAgg, all_m, all_d));
+            int j = (int)blk - 1;  // the window's nearest predecessor
+            uint32_t spins = 0;
+            while (j >= 0) {  // uniform
+                const int idx = j - lane;
+                const uint64_t w = idx >= 0 ? lb_load(&lb.st[idx]) : kLbInc;  // before workgroup 0: zero
+                const uint32_t flag = (uint32_t)(w >> 62);
+                const uint64_t inc = __builtin_amdgcn_ballot_w64(flag == 2u);
+                const uint64_t notready = __builtin_amdgcn_ballot_w64(flag == 0u);
+                const int fp = inc ? __builtin_ctzll(inc) : 63;  // lanes 0..fp are needed
+                const uint64_t need = fp == 63 ? ~0ull : ((2ull << fp) - 1ull);
+                if (notready & need) {
+                    if (++spins > kLbSpinLimit) {
+                        fail = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                exm += wave_sum(lane <= fp ? (uint32_t)w & 0x7fffffffu : 0u);
+                exd += wave_sum(lane <= fp ? (uint32_t)(w >> 31) & 0x7fffffffu : 0u);
+                if (inc) break;
+                j -= 64;
+            }
+            if (lane == 0) lb_store(&lb.st[blk], lb_word(kLbInc, exm + all_m, exd + all_d));
+        }
+        if (lane == 0) {
+            s_off = make_uint2(exm, exd);
+            if (fail && fr.h_totals) fr.h_totals[2] = 2u;  // (never expected) the frame is rendered again
+            if (blk == nblocks - 1) {  // the last workgroup: the frame's (V, D)
+                // the device count holds the duplicates emitted (below cap: a frame that did not fit
+                // is detected by the host from the pinned count, and rendered again), so every
+                // entry the sort and the blend read was written
+                fr.totals[0] = exm + all_m;
+                fr.totals[1] = min(exd + all_d, cap > dup_base ? cap - dup_base : 0u);
+                if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
+                    fr.h_totals[0] = exm + all_m;
+                    fr.h_totals[1] = exd + all_d;
+                    if (!fail) fr.h_totals[2] = 0;  // the prefix-sort miss flag (k_draw)
+                    fr.h_totals[3] = 0;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t run_m = s_off.x + wm, run_d = s_off.y + wd;
+    // the emission (k_emit's, from the records in LDS; duplicates at dup_base)
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+        const Rec raw = wrec[it * 64 + lane];
+        int4 rc;
+        if constexpr (PACK) rc = unpack_rec(raw);
+        else rc = raw;
+        const uint64_t hm = __builtin_amdgcn_ballot_w64(rc.y >= 0);
+        const int i = wbase + it * 64 + lane;
+        if (rc.y >= 0) {
+            // :153-155 uint tileIndex = tileY*16 + tileX; key = tileIndex + projectedMean.z
+            const uint32_t mpos = run_m + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+            const uint32_t key = f2u((float)((uint32_t)rc.z * 16u + (uint32_t)rc.y) + u2f((uint32_t)rc.x));
+            if (mpos < cap) {
+                keys[mpos] = key;
+                vals[mpos] = (uint32_t)i;
+            }
+            // prefix sort: one main in kPrefixSample (by position) into the sampled histogram
+            if (phist && (mpos % kPrefixSample) == 0 && key_class(key) < 256u) {
+                const uint32_t c = key_class(key);
+                atomicAdd(&phist[((size_t)((mpos / kPrefixSample) % kPrefixHistCopies) * 256 + c) * kPrefixBuckets +
+                                 prefix_slot(prefix_bucket(class_hi(c) - key))],
+                          1u);
+            }
+        }
+        run_m += (uint32_t)__popcll(hm);
+        const uint16_t *incl = s_incl[wid][it];
+        const uint32_t T = incl[63];
+        if (T) {  // uniform per wave: this item's duplicates [run_d, + T) of the duplicate range
+            const int ibase = wbase + it * 64;
+            for (uint32_t e0 = 0; e0 < T; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                int s = 0;  // owner: first lane with incl > e
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (incl[s + step - 1] <= e) s += step;
+                const uint32_t q = e - (s ? (uint32_t)incl[s - 1] : 0u);  // index in the owner's walk
+                int4 r;
+                if constexpr (PACK) r = unpack_rec(wrec[it * 64 + s]);
+                else r = wrec[it * 64 + s];
+                const int rx0 = r.w & 0xff, rx1 = (r.w >> 8) & 0xff, ry0 = (r.w >> 16) & 0xff, ry1 = (r.w >> 24) & 0xff;
+                const int w = rx1 - rx0 + 1;
+                // walk position, skipping the main tile if it lies in the rect
+                const bool mainIn = r.y >= rx0 && r.y <= rx1 && r.z >= ry0 && r.z <= ry1;
+                const uint32_t mpos_walk = (uint32_t)((r.z - ry0) * w + (r.y - rx0));
+                const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
+                // k / w for k < 256, 1 <= w <= 16 (k_emit)
+                const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(w, 1)));
+                const uint32_t dx = k - dy * (uint32_t)w;
+                const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
+                const uint32_t key = f2u((float)tile + u2f((uint32_t)r.x));
+                const uint32_t dd = run_d + e;  // place in the duplicate range
+                if (e < T && dup_base + dd < cap) {
+                    keys[dup_base + dd] = key;
+                    vals[dup_base + dd] = (uint32_t)(ibase + s);
+                }
+                if (phist && e < T && (dd % kPrefixSample) == 0 && key_class(key) < 256u) {
+                    const uint32_t c = key_class(key);
+                    atomicAdd(&phist[((size_t)((dd / kPrefixSample) % kPrefixHistCopies) * 256 + c) * kPrefixBuckets +
+                                     prefix_slot(prefix_bucket(class_hi(c) - key))],
+                              1u);
+                }
+            }
+        }
+        run_d += T;
     }
 }
 
@@ -775,7 +1009,12 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_DRAW_WAVES
 #define GS_DRAW_WAVES 7
 #endif
-template <bool FAST_EXP, bool STATS>
+// SMALL: the small-frame form -- 8x8 sub-blocks, one pixel per lane with its state in registers
+// from the start (the sparse phase's survivor step throughout): four times the waves of the
+// 16x16 form on the same image, each walking its tile's list for 64 pixels.  Frames whose blend
+// is latency-bound (a few thousand short-lived sub-blocks, C2 / the small C5 views) take it; a
+// pixel's arithmetic and its survivor order are the same, so the image is the same bit for bit.
+template <bool FAST_EXP, bool STATS, bool SMALL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVES))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
                                              const uint2 *__restrict__ cullbox,
@@ -784,11 +1023,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                                              uint32_t *fr_h_totals) {
     // pixel state, pixel id = 16*y + x in the sub-block; a pixel is done (:129-133) iff its
     // w >= 0.99 (pixels outside the image start at w = 1)
-    __shared__ float4 s_col[256];
+    constexpr int SB = SMALL ? 8 : 16;  // sub-block side
+    __shared__ float4 s_col[SMALL ? 1 : 256];
     // one survivor's blend events: power and pixel id (split); 5760 B of LDS per wave in all
     // -> 7 waves/SIMD
-    __shared__ __attribute__((aligned(16))) float s_epow[256];
-    __shared__ uint8_t s_epix[256];
+    __shared__ __attribute__((aligned(16))) float s_epow[SMALL ? 1 : 256];
+    __shared__ uint8_t s_epix[SMALL ? 1 : 256];
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
@@ -822,9 +1062,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int tx = t & 15, ty = t >> 4;
     const int sby = sub / P.nbx, sbx = sub - sby * P.nbx;
     const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
-    const int x0 = P.xb[tx] + sbx * 16, y0 = P.yb[ty] + sby * 16;
+    const int x0 = P.xb[tx] + sbx * SB, y0 = P.yb[ty] + sby * SB;
     if (x0 >= xe || y0 >= ye) return;  // uniform: sub-block beyond this tile
-    const int x1 = min(x0 + 16, xe), y1 = min(y0 + 16, ye);
+    const int x1 = min(x0 + SB, xe), y1 = min(y0 + SB, ye);
     const int lane = threadIdx.x;
     const int pxa = x0 + 2 * (lane & 7), pya = y0 + 2 * (lane >> 3);
     const bool in00 = pxa < x1 && pya < y1, in10 = pxa + 1 < x1 && pya < y1;
@@ -857,10 +1097,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // pixel ids are row-major in the sub-block (16 * y + x): the lane's quad is qbase + kQuad[k]
     const uint32_t qbase = 32u * ((uint32_t)lane >> 3) + 2u * ((uint32_t)lane & 7u);
     constexpr uint32_t kQuad[4] = {0u, 1u, 16u, 17u};
+    if constexpr (!SMALL) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const bool dk = k == 0 ? d00 : k == 1 ? d10 : k == 2 ? d01 : d11;
-        s_col[qbase + kQuad[k]] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
+        for (int k = 0; k < 4; ++k) {
+            const bool dk = k == 0 ? d00 : k == 1 ? d10 : k == 2 ? d01 : d11;
+            s_col[qbase + kQuad[k]] = make_float4(0.f, 0.f, 0.f, dk ? 1.0f : 0.0f);
+        }
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_refresh = 0;
@@ -932,8 +1174,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         pc = s_col[spix];  // stays in registers to the end (written back once)
         sparse = true;
     };
-    // blocks with few pixels in the image start sparse
-    if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) go_sparse();
+    if constexpr (SMALL) {  // one pixel per lane, (x0 + lane % 8, y0 + lane / 8), from the start
+        SA = ballot(x0 + (lane & 7) < x1 && y0 + (lane >> 3) < y1);
+        nact = 64;
+        spix = (uint32_t)(lane & 7) | ((uint32_t)(lane >> 3) << 4);  // (x, y) offsets as 16 * y + x
+        sparse = true;
+        all_done = SA == 0;
+    } else {
+        // blocks with few pixels in the image start sparse
+        if (!all_done && 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3) <= 64) go_sparse();
+    }
 
     // The list streams through a three-stage pipeline, one 64-entry chunk per step; chunk c:
     //   step c-2: index load (coalesced)   step c-1: box gather   step c: box test
@@ -969,9 +1219,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         const int q = p < cpos ? p : p < cpos + cn ? -1 : p - cn;
         v = *at(vals_m1, (uint32_t)(min(q, qmax) + 1) << 2);
     };
+    // (ids clamped to the scene: the gathers stay inside the per-splat buffers whatever a frame's
+    // values hold -- the clamp sits here, where the index load has arrived, not at the load)
+    const uint32_t idmax = (uint32_t)max(P.n - 1, 0);
     auto gather_box = [&](uint32_t v, uint32_t &vb, uint2 &bx) {
-        vb = v;
-        bx = *at(cullbox, v << 3);
+        vb = min(v, idmax);
+        bx = *at(cullbox, vb << 3);
     };
     // box test of a chunk; its survivors join the queue
     auto test_and_queue = [&](int cbase, uint32_t v, const uint2 &bx) __attribute__((always_inline)) {
@@ -1217,8 +1470,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // channels are never -0, and x + (+-0) == x otherwise); a non-finite colour (inf * 0 is
         // NaN) keeps the selects.
         cfin = ballot(!(__builtin_isfinite(Dc.x) & __builtin_isfinite(Dc.y) & __builtin_isfinite(Dc.z))) == 0;
-        if (!sparse && blend_dense(bk, Dd, Dc)) go_sparse();
-        if (sparse) blend_sparse(bk, Dd, Dc);
+        if constexpr (SMALL) {
+            blend_sparse(bk, Dd, Dc);
+        } else {
+            if (!sparse && blend_dense(bk, Dd, Dc)) go_sparse();
+            if (sparse) blend_sparse(bk, Dd, Dc);
+        }
         inflight = false;
     };
     // prologue: chunk 0 index-loaded and box-gathered, chunk 1 index-loaded
@@ -1250,6 +1507,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         }
     }
     if (P.prefix && end < wend && !all_done && fr_h_totals) fr_h_totals[2] = 1u;  // (uniform) a prefix miss
+    if constexpr (SMALL) {  // the lane's pixel (coordinates again from the lane id, see below)
+        const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int qx = x0 + (l2 & 7), qy = y0 + (l2 >> 3);
+        if (qx < x1 && qy < y1) out[(size_t)qy * P.W + qx] = pack_rgba8(pc);
+    } else {
     if (sparse && (uint32_t)lane < nact) s_col[spix] = pc;  // the sparse phase's state (distinct pixels)
     wave_lds_sync();
     {  // the quad's pixels again from the lane id (v_mbcnt, which the compiler does not merge with
@@ -1263,6 +1525,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + 1]);
         if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + 16]);
         if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + 17]);
+    }
     }
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -1296,15 +1559,22 @@ int preprocess_blocks(int n) { return (n + kSplatsPerBlock - 1) / kSplatsPerBloc
 // separate hipEventRecord costs an idle gap of several microseconds on the stream.
 bool rec_packed(const PreParams &P) { return P.clean || (P.W >= 16 && P.H >= 16); }
 
-void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start) {
+void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
+                       bool lazy) {
     const int nb = preprocess_blocks(P.n);
     if (nb <= 0) return;
-    if (P.clean)  // (clean mode always packs its records)
-        hipExtLaunchKernelGGL((k_preprocess<true, true>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
-    else if (rec_packed(P))
-        hipExtLaunchKernelGGL((k_preprocess<true, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
-    else
-        hipExtLaunchKernelGGL((k_preprocess<false, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr);
+#define GS_PRE(PK, CL, LZ) \
+    hipExtLaunchKernelGGL((k_preprocess<PK, CL, LZ>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr)
+    if (P.clean) {  // (clean mode always packs its records)
+        if (lazy) GS_PRE(true, true, true);
+        else GS_PRE(true, true, false);
+    } else if (rec_packed(P)) {
+        if (lazy) GS_PRE(true, false, true);
+        else GS_PRE(true, false, false);
+    } else {
+        GS_PRE(false, false, false);
+    }
+#undef GS_PRE
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
@@ -1318,6 +1588,32 @@ void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t
     else hipExtLaunchKernelGGL(k_emit<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, prefix_hist);
 }
 
+void launch_pre_emit(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const LookbackDev &lb,
+                     bool lazy, uint32_t *keys, uint32_t *vals, uint32_t cap, uint32_t *prefix_hist, hipEvent_t start,
+                     hipEvent_t stop) {
+    const uint32_t nb = (uint32_t)preprocess_blocks(P.n);
+    if (nb == 0) {  // no splats: no entries
+        hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, 0);
+        return;
+    }
+    const uint32_t dup_base = (uint32_t)P.n;
+#define GS_PE(PK, CL, LZ)                                                                                          \
+    hipExtLaunchKernelGGL((k_pre_emit<PK, CL, LZ>), dim3(nb), dim3(kBlock), 0, s, start, stop, 0, P, sc, fr, lb, keys, \
+                          vals, cap, dup_base, prefix_hist, nb)
+    const bool packed = rec_packed(P);
+    if (P.clean) {
+        if (lazy) GS_PE(true, true, true);
+        else GS_PE(true, true, false);
+    } else if (packed) {
+        if (lazy) GS_PE(true, false, true);
+        else GS_PE(true, false, false);
+    } else {
+        if (lazy) GS_PE(false, false, true);
+        else GS_PE(false, false, false);
+    }
+#undef GS_PE
+}
+
 void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t *dev_count, uint32_t *counts,
                  uint32_t *bins, hipEvent_t stop) {
     const int64_t per = (int64_t)kBlock * kBinItems;
@@ -1327,23 +1623,28 @@ void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t 
     hipExtLaunchKernelGGL(k_bins_scan, dim3(1), dim3(kBlock), 0, s, nullptr, stop, 0, counts, bins);
 }
 
-void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, const uint32_t *bins, const uint32_t *vals,
-                 const FrameDev &fr, const float4 *colour, uint32_t *out, unsigned long long *stats, hipEvent_t start,
-                 hipEvent_t stop) {
-    // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks, XCD-major (see k_draw), then the
-    // margin blocks (256 uncovered pixels each); with no coverage only margin blocks run
+void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, bool small, const uint32_t *bins,
+                 const uint32_t *vals, const FrameDev &fr, const float4 *colour, uint32_t *out,
+                 unsigned long long *stats, hipEvent_t start, hipEvent_t stop) {
+    // 1-D grid: 256 tiles x (nbx*nby) one-wave sub-blocks (16x16, or 8x8 when small), XCD-major
+    // (see k_draw), then the margin blocks (256 uncovered pixels each); with no coverage only
+    // margin blocks run
     const int margin = P.W * P.H - P.coverW * P.coverH;
     const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
-#define GS_DRAW(F, S)                                                                                         \
-    hipExtLaunchKernelGGL((k_draw<F, S>), grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, \
+#define GS_DRAW(F, S, M)                                                                                         \
+    hipExtLaunchKernelGGL((k_draw<F, S, M>), grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, \
                           colour, out, stats, fr.h_totals)
+#define GS_DRAW2(F, S) \
+    if (small) GS_DRAW(F, S, true); \
+    else GS_DRAW(F, S, false)
     if (stats) {
-        if (fast_exp) GS_DRAW(true, true);
-        else GS_DRAW(false, true);
+        if (fast_exp) GS_DRAW2(true, true);
+        else GS_DRAW2(false, true);
     } else {
-        if (fast_exp) GS_DRAW(true, false);
-        else GS_DRAW(false, false);
+        if (fast_exp) GS_DRAW2(true, false);
+        else GS_DRAW2(false, false);
     }
+#undef GS_DRAW2
 #undef GS_DRAW
 }
 

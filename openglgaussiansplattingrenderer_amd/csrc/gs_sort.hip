@@ -146,11 +146,19 @@ __host__ __device__ constexpr uint32_t xcd_grid(uint32_t nb) { return 8 * ((nb +
 // PREFIX (the first pass of a frame's prefix sort): only the keys at or below their class
 // bound (PrefixDev::theta) are counted for the digits; the tile counts (TILES) stay over every
 // key; the kept keys per class and the keys below 1.0 (class 0's total) go to pre.counts
+// dup_base (the first pass of a frame sort after k_pre_emit, else kNoSplit): the input is the
+// emission's split layout -- element i < V at i, element i >= V at i - V + dup_base (V = cnt[0])
+constexpr uint32_t kNoSplit = 0xffffffffu;
+__device__ __forceinline__ uint32_t split_at(uint32_t idx, uint32_t v0, uint32_t gap) {
+    return idx >= v0 ? idx + gap : idx;
+}
+
 template <int W, bool TILES, bool PREFIX = false>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
-                                                    uint32_t *__restrict__ tile_counts, PrefixDev pre) {
+                                                    uint32_t *__restrict__ tile_counts, PrefixDev pre,
+                                                    uint32_t dup_base, uint32_t *__restrict__ zero_cols) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems;
     static_assert(kThreads >= kRadix, "one thread per digit flushes the counts");
     const uint32_t n = elem_count(n_max, cnt);
@@ -179,7 +187,14 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems];
-    if (tile * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
+    if (dup_base != kNoSplit) {  // uniform: the split emission layout
+        const uint32_t v0 = cnt[0], gap = dup_base - v0;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t idx = base + k * 64;
+            kk[k] = (idx < n) ? keys[split_at(idx, v0, gap)] : 0u;
+        }
+    } else if (tile * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
         const uint32_t *p = keys + base;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) kk[k] = p[k * 64];
@@ -237,6 +252,10 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     const int d = threadIdx.x;
     if (d >= kRadix) return;
     hist[(size_t)d * nb + tile] = sum8(&s_cnt[d * kRep]);
+    if (zero_cols) {  // the small sort: this tile's columns of passes 1-3 (k_sweep_small adds into them)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) zero_cols[((size_t)q * kRadix + d) * nb + tile] = 0u;
+    }
     if (TILES) {
         const uint32_t c = sum8(&s_tiles[d * kRep]);
         if (c) atomicAdd(&tile_counts[(blockIdx.x % kTileCopies) * kRadix + d], c);
@@ -449,7 +468,8 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
                                                       const uint32_t *__restrict__ hist, uint32_t nb,
-                                                      const uint32_t *__restrict__ row_total, PrefixDev pre) {
+                                                      const uint32_t *__restrict__ row_total, PrefixDev pre,
+                                                      uint32_t dup_base) {
     constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
     static_assert(kThreads >= kRadix, "one thread per digit scans the counts");
     const uint32_t n = elem_count(n_max, cnt);
@@ -474,7 +494,16 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     const uint32_t tile0 = tile * (uint32_t)kTile;
     const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems], vv[kItems];
-    if (tile0 + kTile <= n) {  // uniform: full tile, immediate offsets
+    if (dup_base != kNoSplit) {  // uniform: the split emission layout (see k_upsweep)
+        const uint32_t v0 = cnt[0], gap = dup_base - v0;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t idx = base + k * 64;
+            const uint32_t a = split_at(idx, v0, gap);
+            kk[k] = (idx < n) ? kin[a] : 0u;
+            vv[k] = (FMT != kPackIn && idx < n) ? vin[a] : 0u;
+        }
+    } else if (tile0 + kTile <= n) {  // uniform: full tile, immediate offsets
         const uint32_t *pk = kin + base, *pv = vin + base;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
@@ -609,6 +638,134 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     }
 }
 
+// ------------------------------------------------------------ small sorts (few tiles)
+// A frame with few entries (C2: 51k; the small C5 views: 0.2-1M) is latency-bound: each of the
+// 12 launches of the reduce-then-scan sort costs ~4-10 us of dispatch and memory round trips
+// for a handful of workgroups.  The small form runs 8: per pass the histogram (k_upsweep) and
+// one k_sweep_small, which computes its tile's digit offsets itself from the pass's histogram
+// rows (thread d sums row d: its total, and its tiles before this one; a block scan of the
+// totals gives the digit bases) -- k_scan_rows' work, O(tiles) reads per thread, cheap for few
+// tiles -- then ranks and scatters like k_downsweep.  (Counting the next pass's histogram in
+// the sweep with global atomics instead of an upsweep launch was measured: the top-byte pass's
+// few digits put ~800 cross-XCD atomics on each counter, 0.45 ms for the 51k-entry C2 sort.)
+// Any entry count is sorted correctly; the host picks this form for frames whose previous count
+// was small (kSmallSortEntries).  Tiles of 4096 keys (4 waves).
+__global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t *__restrict__ kin,
+                                                               const uint32_t *__restrict__ vin,
+                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                               uint32_t n_max, const uint32_t *__restrict__ cnt,
+                                                               int shift, const uint32_t *__restrict__ hist, uint32_t nb,
+                                                               uint32_t dup_base, uint32_t *__restrict__ tile_counts,
+                                                               uint32_t *__restrict__ bins) {
+    constexpr int kThreads = kWaveSmall * 64, kTile = kThreads * kItems, kWaves = kWaveSmall;
+    static_assert(kThreads == kRadix, "one thread per digit");
+    __shared__ uint32_t s_w[4];
+    if (bins && blockIdx.x == gridDim.x - 1) {  // uniform: the bins workgroup (first pass)
+        __shared__ uint32_t s_above;
+        bins_scan(tile_counts, bins, s_w, &s_above);
+        return;
+    }
+    const uint32_t n = elem_count(n_max, cnt);
+    const uint32_t live = (n + kTile - 1) / kTile;
+    const uint32_t tile = blockIdx.x;
+    if (tile >= live) return;  // uniform
+    __shared__ uint32_t s_cnt[kWaves][kRadix];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ int32_t s_gbase[kRadix];
+    __shared__ uint32_t s_wave[kWaves];
+    __shared__ uint32_t s_keys[kTile];
+    __shared__ uint32_t s_vals[kTile];
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t tile0 = tile * (uint32_t)kTile;
+    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems];
+    {
+        const uint32_t v0 = dup_base != kNoSplit ? cnt[0] : 0xffffffffu, gap = dup_base - v0;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t idx = base + k * 64;
+            const uint32_t a = split_at(idx, v0, gap);
+            kk[k] = (idx < n) ? kin[a] : 0u;
+            vv[k] = (idx < n) ? vin[a] : 0u;
+        }
+    }
+    // the digit offsets, while the keys load: thread d sums hist row d (the tiles before this one,
+    // and all of them)
+    // (rows are nb words, nb a multiple of 4: 16-byte loads, 64 tiles per round trip)
+    const int d = threadIdx.x;
+    uint32_t before = 0, total = 0;
+    {
+        const uint4 *row = reinterpret_cast<const uint4 *>(hist + (size_t)d * nb);
+        for (uint32_t j = 0; j < live; j += 64) {
+            uint4 v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = (j + 4 * q < live) ? row[(j >> 2) + q] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const uint32_t t0 = j + 4 * q;
+                const uint32_t c[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t x = (t0 + r < live) ? c[r] : 0u;  // columns of tiles past the count are stale
+                    total += x;
+                    before += (t0 + r < tile) ? x : 0u;
+                }
+            }
+        }
+    }
+    uint32_t rank[kItems], lead[kItems], old[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const bool valid = base + k * 64 < n;
+        const uint32_t dg = (kk[k] >> shift) & 0xffu;
+        const uint64_t m = match_digit(dg, __ballot(valid));
+        rank[k] = count_below(m);
+        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
+        old[k] = valid ? (uint32_t)__popcll(m) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const bool valid = base + k * 64 < n;
+        if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    __syncthreads();
+    {
+        uint32_t tot = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            const uint32_t c = s_cnt[w][d];
+            s_cnt[w][d] = tot;
+            tot += c;
+        }
+        const uint32_t start = block_excl_scan<kWaves>(tot, s_wave);
+        const uint32_t gdig = block_excl_scan<kWaves>(total, s_wave);  // digit base, whole array
+        s_start[d] = start;
+        s_gbase[d] = (int32_t)(gdig + before) - (int32_t)start;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        if (base + k * 64 < n) {
+            const uint32_t dg = (kk[k] >> shift) & 0xffu;
+            const uint32_t pos = s_start[dg] + s_cnt[wid][dg] + rank[k];
+            s_keys[pos] = kk[k];
+            s_vals[pos] = vv[k];
+        }
+    }
+    __syncthreads();
+    const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
+    for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
+        const uint32_t key = s_keys[i];
+        const uint32_t o = (uint32_t)(s_gbase[(key >> shift) & 0xffu] + (int32_t)i);
+        kout[o] = key;
+        vout[o] = s_vals[i];
+    }
+}
+
 // The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
 // [8j, 8j + 8) of every copy): walking the sampled histogram from the largest distance (the
 // front of the list) down, the bucket where the count reaches target / kPrefixSample sets
@@ -665,8 +822,9 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 }  // namespace
 
-int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s) {
-    const size_t nb = (size_t)((n + kTileSmall - 1) / kTileSmall);  // the most tiles of any pass
+int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small) {
+    // the most tiles of any pass (the small form keeps all four passes' histograms)
+    const size_t nb = (size_t)((n + kTileSmall - 1) / kTileSmall) + 3;  // (+3: the small form's 16-byte rows)
     const bool grow_alt = (size_t)n > sc.alt_cap, grow_hist = nb * kRadix > sc.hist_cap;
     if ((grow_alt && sc.keys_alt) || (grow_hist && sc.hist)) (void)hipStreamSynchronize(s);  // in-flight users
     if (grow_alt) {
@@ -711,7 +869,12 @@ void sort_free(SortScratch &sc) {
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out,
-               const PrefixDev *pre) {
+               const PrefixDev *pre, int64_t dup_base, bool small) {
+    if (dup_base >= 0 && !dev_count) {
+        err = "radix sort: the split layout needs a device count";
+        return GS_ERR_INVALID;
+    }
+    small = small && !pre && n >= 1;
     if (pre && (!bins || !dev_count)) {
         err = "radix sort: a prefix sort needs bins and a device count";
         return GS_ERR_INVALID;
@@ -725,7 +888,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         err = "radix sort: n must be < 2^31";
         return GS_ERR_INVALID;
     }
-    int rc = sort_ensure(sc, std::max<int64_t>(n, 1), err, s);
+    int rc = sort_ensure(sc, std::max<int64_t>(n, 1), err, s, small);
     if (rc) return rc;
     uint32_t *tile_counts = sc.row_total + kRadix;
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
@@ -734,6 +897,34 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
                            tile_counts, bins, PrefixDev{}, 0);
         if (stop) (void)hipEventRecord(stop, s);
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
+    }
+    if (small) {  // the small form (k_sweep_small): 8 launches, keys and values out
+        const uint32_t nb = (uint32_t)((n + kTileSmall - 1) / kTileSmall + 3) & ~3u;  // row stride: 16-byte rows
+        const uint32_t split = dup_base >= 0 ? (uint32_t)dup_base : kNoSplit;
+        uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint32_t sp = pass == 0 ? split : kNoSplit;
+            hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
+            if (pass == 0 && bins)
+                hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, true>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0,
+                                      nullptr, 0, kin, (uint32_t)n, dev_count, 0, sc.hist, nb, tile_counts, PrefixDev{},
+                                      sp, nullptr);
+            else
+                hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0,
+                                      nullptr, 0, kin, (uint32_t)n, dev_count, 8 * pass, sc.hist, nb, nullptr,
+                                      PrefixDev{}, sp, nullptr);
+            const dim3 grid(nb + ((pass == 0 && bins) ? 1 : 0));
+            hipExtLaunchKernelGGL(k_sweep_small, grid, dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin, vin, kout, vout,
+                                  (uint32_t)n, dev_count, 8 * pass, sc.hist, nb, sp, tile_counts,
+                                  pass == 0 ? bins : nullptr);
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        if (hipGetLastError() != hipSuccess) {
+            err = "radix sort: kernel launch failed";
+            return GS_ERR_HIP;
+        }
+        return GS_OK;
     }
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     PrefixDev pd = pre ? *pre : PrefixDev{};
@@ -753,18 +944,20 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const uint32_t nb = (uint32_t)((np + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
+        // the first pass reads the split emission layout (dup_base >= 0), the others their own output
+        const uint32_t split = (pass == 0 && dup_base >= 0) ? (uint32_t)dup_base : kNoSplit;
         if (big && pre)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split, nullptr);
         else if (big && bins)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split, nullptr);
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split, nullptr);
         else
             hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, kNoSplit, nullptr);
         // one more workgroup scans the tile counts in the last pass (a prefix sort: with the draw
         // limits; and one in the first pass makes the class tables passes 1-3 need)
         const bool with_bins = bins && (pass == 3 || (pre && pass == 0));
@@ -776,22 +969,22 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
         if (big && pre)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (big)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
-                                  kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (fmt == kPairs)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
-                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (fmt == kPlace)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
-                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (fmt == kPackOut)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackOut>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackIn>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
-                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd);
+                                  e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

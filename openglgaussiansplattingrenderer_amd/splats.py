@@ -61,6 +61,19 @@ class Context:
         check(lib().gs_ctx_set_sort_prefix(self.handle, int(target), ctypes.byref(cur)), self.handle)
         return cur.value
 
+    def set_small_limits(self, draw_entries: int = -1, sort_entries: int = -1):
+        """gs_ctx_set_small_limits: entry counts below which frames blend in 8x8 sub-blocks /
+        sort in 8 launches (-1 leaves a limit)"""
+        check(lib().gs_ctx_set_small_limits(self.handle, int(draw_entries), int(sort_entries)), self.handle)
+
+    def set_draw_sub(self, sub: int = -1) -> int:
+        """the blend's sub-block form (gs_ctx_set_draw_sub): 0 by entry count (default), 8 (one
+        pixel per lane, small frames) or 16 (2x2 quads per lane, large frames); -1 leaves it.
+        Returns the form the newest frame's blend used (0 before any)."""
+        cur = ctypes.c_int()
+        check(lib().gs_ctx_set_draw_sub(self.handle, int(sub), ctypes.byref(cur)), self.handle)
+        return cur.value
+
     def prefix_stats(self, reset: bool = False) -> dict:
         """gs_prefix_stats: frames prefix-sorted, of them rendered again, entries kept / entries of
         the newest retired prefix-sorted frame"""

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <thread>
 #include <vector>
 
 #include "gsplat_splats.hpp"
@@ -93,6 +94,16 @@ int main(int argc, char **argv) {
         const std::vector<uint8_t> img = splats.display();
         std::ofstream(argv[2], std::ios::binary).write((const char *)img.data(), (std::streamsize)img.size());
         std::cout << "rendered C1: duplicates " << splats.numDuplicates << std::endl;
+    }
+    {  // a Context made current here and destroyed on another thread is no longer current here
+        gs::Context *other = new gs::Context(0);
+        other->makeCurrent();
+        EXPECT(gs::Context::current() == other);
+        std::thread([other] { delete other; }).join();
+        EXPECT(gs::Context::current() == nullptr);
+        EXPECT(gs::GPURadixSort(1u, 3u, 2u, nullptr, nullptr, nullptr, 0, 16, 32, nullptr) == GS_ERR_STATE);
+        ctx.makeCurrent();
+        EXPECT(gs::Context::current() == &ctx);
     }
     std::cout << "ALL PASSED" << std::endl;
     return 0;

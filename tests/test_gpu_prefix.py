@@ -109,6 +109,7 @@ def test_prefix_off_and_stage_calls():
     img = ref.download(np.uint8, W * H * 4)
     E = int(st.entries)
     vals_full = sp.read(g.GS_READ_VALS, E)
+    bins_full = sp.read(g.GS_READ_BINS, 256)
     ctx.set_sort_prefix(0)
     ctx.prefix_stats(reset=True)
     out = g.DeviceBuffer(ctx, W * H * 4)
@@ -129,4 +130,143 @@ def test_prefix_off_and_stage_calls():
     assert np.array_equal(sp.read(g.GS_READ_VALS, E), vals_full)
     check(lib().gs_sort(ctx.handle), ctx.handle)
     assert np.array_equal(sp.read(g.GS_READ_VALS, E), vals_full)
+    # gs_compute_bins right after a frame whose sort left the keys unsorted: the entries are sorted
+    # again with their keys first
+    render_spec(sp, u, out)
+    check(lib().gs_compute_bins(ctx.handle), ctx.handle)
+    assert np.array_equal(sp.read(g.GS_READ_BINS, 256), bins_full)
+    ctx.set_sort_prefix(0)
+    render_spec(sp, u, out)
+    check(lib().gs_compute_bins(ctx.handle), ctx.handle)
+    assert np.array_equal(sp.read(g.GS_READ_BINS, 256), bins_full)
+    assert np.array_equal(sp.read(g.GS_READ_VALS, E), vals_full)
+    ctx.close()
+
+
+def sheet_and_cluster_scene(u, n_cluster, seed):
+    """an opaque sheet of splats in front of the camera covering the whole image (every pixel
+    saturates within the first entries of its tile's list), behind it a tight cluster of n_cluster
+    splats around the world origin (a few tile lists of ~n_cluster entries): a frame that sorts
+    only ~32k entries of each list deep and never misses, and keeps few entries in all"""
+    rng = np.random.default_rng(seed)
+    W, H = u.width, u.height
+    VP = np.array(u.vp[:], np.float64).reshape(4, 4).T
+    V = np.array(u.view[:], np.float64).reshape(4, 4).T
+    gx, gy = np.meshgrid(np.arange(-60, W + 61, 24.0), np.arange(-60, H + 61, 24.0))
+    ndc = np.stack([2 * gx.ravel() / W - 1, 2 * gy.ravel() / H - 1, np.full(gx.size, 0.9), np.ones(gx.size)], 1)
+    wpt = (np.linalg.inv(VP) @ ndc.T).T
+    sheet = wpt[:, :3] / wpt[:, 3:]
+    depth = -(V @ np.c_[sheet, np.ones(len(sheet))].T)[2]  # view-space distance
+    sig = 30.0 * depth / u.focal_y  # ~30 px
+    n_s = len(sheet)
+    cl = rng.normal(0.0, 0.05, (n_cluster, 3))
+    means = np.r_[sheet, cl].astype(np.float32)
+    q = rng.normal(size=(n_s + n_cluster, 4)).astype(np.float32)
+    q[:n_s] = [1, 0, 0, 0]
+    rot = q / np.linalg.norm(q, axis=1, keepdims=True)
+    log_sc = np.r_[np.repeat(np.log(sig)[:, None], 3, 1), np.full((n_cluster, 3), -5.0)].astype(np.float32)
+    op = np.r_[np.full(n_s, 10.0), rng.normal(0.0, 2.0, n_cluster)].astype(np.float32)  # logits
+    col = rng.normal(0.0, 0.8, (n_s + n_cluster, 3)).astype(np.float32)
+    return means, col, op, log_sc, rot
+
+
+def test_prefix_full_fallback_renders_again():
+    """a prefix-sorted frame that keeps more entries than its passes 1-3 were sized for
+    (the previous prefix frame's kept count + 25 % + 64Ki) sorts only part of its kept keys; it is
+    flagged and rendered again with the full sort.  Scene A (an opaque sheet in front of a tight
+    cluster: a few deep lists, every pixel saturating early)
+    keeps ~0.2M entries, then scene B (the C3 stand-in) keeps ~2.2M in the same context: B's
+    first prefix frame takes the `full` path.  Its image equals the host-synchronous frame's."""
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    ctx.set_lanes(1)  # one lane: the entry buffers B's sync frame grows are the ones B's frame uses
+    assert ctx.set_sort_prefix() == 32768
+    u = g.main_camera(W, H).uniforms()
+    spa = g.Splats.from_raw(*sheet_and_cluster_scene(u, 2_300_000, 8), W, H, ctx=ctx)
+    spb = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    stb = render_sync(spb, u, ref)  # B's entries sized; the host now knows an entry count
+    img_b = ref.download(np.uint8, W * H * 4)
+    sta = render_sync(spa, u, ref)
+    img_a = ref.download(np.uint8, W * H * 4)
+    assert sta.entries >= 64 * 32768, sta.entries  # A's frames are prefix-sorted
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    ctx.prefix_stats(reset=True)
+    for _ in range(2):
+        render_spec(spa, u, out)
+    ctx.sync()
+    psa = ctx.prefix_stats(reset=True)
+    assert psa["frames"] == 2 and psa["redone"] == 0, psa
+    assert np.array_equal(out.download(np.uint8, W * H * 4), img_a)
+    kept_a = psa["kept"]
+    render_spec(spb, u, out)  # sized for A's kept count: too small for B's
+    ctx.sync()
+    psb = ctx.prefix_stats()
+    assert psb["frames"] == 1 and psb["redone"] == 1, psb
+    assert psb["kept"] > kept_a * 5 // 4 + 65536, (kept_a, psb)  # the `full` case, not a miss
+    assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
+    # the next B frame is sized from B's kept count: no redo
+    render_spec(spb, u, out)
+    ctx.sync()
+    assert ctx.prefix_stats()["redone"] == 1
+    assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
+    ctx.close()
+
+
+def test_prefix_depth_decays_after_clean_frames():
+    """misses double the depth; 64 frames in a row without a miss halve it again, never
+    below the configured target -- misses do not deepen the sort (or turn it off: E < 64 * target)
+    for good."""
+    W, H = 1280, 720
+    ctx = g.Context(0)
+    sp = g.Splats.from_raw(*bicycle_standin_raw(400_000, seed=3), W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    u = pose(W, H, 0)
+    render_sync(sp, u, ref)
+    img = ref.download(np.uint8, W * H * 4)
+    ctx.set_sort_prefix(256)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    targets = []
+    for _ in range(200):
+        render_spec(sp, u, out)
+        ctx.sync()
+        targets.append(ctx.set_sort_prefix())
+    assert max(targets) > 256, targets[:20]  # 256 entries are too shallow here: misses deepened it
+    drops = sum(1 for a, b in zip(targets, targets[1:]) if b < a)
+    assert drops >= 1, targets  # ... and clean runs brought it down again
+    assert min(targets) >= 256
+    assert np.array_equal(out.download(np.uint8, W * H * 4), img)
+    ctx.close()
+
+
+def test_prefix_on_a_fused_frame():
+    """A scene small enough for the fused preprocess + emission (k_pre_emit: at most 64 workgroups,
+    the split entry layout) with entries enough for the prefix sort (>= 64 * target): the sampled
+    histogram comes from the fused kernel, the sort's first pass reads the split layout -- every
+    frame equals the host-synchronous one (rendered again or not)."""
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    rng = np.random.default_rng(21)
+    n = 60_000
+    means = rng.normal(0.0, 1.5, (n, 3)).astype(np.float32)
+    q = rng.normal(size=(n, 4)).astype(np.float32)
+    rot = q / np.linalg.norm(q, axis=1, keepdims=True)
+    log_sc = rng.uniform(np.log(0.3), np.log(1.2), (n, 3)).astype(np.float32)
+    op = rng.normal(-1.0, 1.5, n).astype(np.float32)
+    col = rng.normal(0.0, 0.8, (n, 3)).astype(np.float32)
+    sp = g.Splats.from_raw(means, col, op, log_sc, rot, W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    for k in range(3):
+        st = render_sync(sp, pose(W, H, k), ref)
+        assert st.entries >= 64 * 32768, st.entries
+    ctx.prefix_stats(reset=True)
+    for k in range(3):
+        render_spec(sp, pose(W, H, k), outs[k])
+    ctx.sync()
+    ps = ctx.prefix_stats()
+    assert ps["frames"] >= 1, ps
+    for k in range(3):
+        render_sync(sp, pose(W, H, k), ref)
+        assert np.array_equal(outs[k].download(np.uint8, W * H * 4), ref.download(np.uint8, W * H * 4)), f"frame {k}"
     ctx.close()

@@ -65,9 +65,17 @@ def assert_image_tol(got, ref, what):
     assert d.max() <= FAST_TOL_MAX and frac >= FAST_TOL_FRAC, f"{what}: max {d.max()} within1 {frac}"
 
 
+@pytest.fixture(params=[16, 8], ids=["sub16", "sub8"])
+def sub(ctx, request):
+    """the blend's sub-block form, forced (gs_ctx_set_draw_sub): both forms give the same image"""
+    ctx.set_draw_sub(request.param)
+    yield request.param
+    ctx.set_draw_sub(0)
+
+
 @pytest.mark.parametrize("name", ["c1", "c2"])
 @pytest.mark.parametrize("mode,flags", [("ref", 0), ("clean", g.GS_FLAG_CLEAN)])
-def test_golden_configs(ctx, golden_dir, name, mode, flags):
+def test_golden_configs(ctx, golden_dir, name, mode, flags, sub):
     z = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
     u = U(z["uniforms"])
     uu = g.make_uniforms(np.array(u.view, np.float32).reshape(4, 4), u.width, u.height, u.focal_x, u.focal_y,
@@ -79,6 +87,7 @@ def test_golden_configs(ctx, golden_dir, name, mode, flags):
     for k in ("means2d", "conics", "keys", "vals", "bins"):
         assert_bits(r[k], z[f"{mode}_{k}"], f"{name}/{mode}/{k}")
     assert_bits(r["image"].reshape(-1), z[f"{mode}_image"].reshape(-1), f"{name}/{mode}/image")
+    assert ctx.set_draw_sub() == sub
     # fast exp: tolerance parity
     rf = gpu_frame(sp, uu, flags | g.GS_FLAG_FAST_EXP)
     assert_image_tol(rf["image"], z[f"{mode}_image"], f"{name}/{mode}/fast")
@@ -87,7 +96,7 @@ def test_golden_configs(ctx, golden_dir, name, mode, flags):
 @pytest.mark.parametrize("W,H,n", [(1920, 1080, 20_000), (3840, 2160, 4_000), (1000, 600, 15_000),
                                    (12, 40, 3_000)])  # 12 px: reference tile width 0 (16-byte records)
 @pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
-def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags):
+def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags, sub):
     """1080p / 4K / odd sizes: Q4 (int vs float tile dims), Q5 (unclamped main tile),
     Q9 (partial coverage) and Q18 (tile-straddling blocks) -- against the oracle live."""
     from openglgaussiansplattingrenderer_amd.scenes import c2_scene
@@ -100,10 +109,11 @@ def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags):
     for k in ("means2d", "conics", "keys", "vals", "bins"):
         assert_bits(r[k], o[k], f"{W}x{H}/{k}")
     assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{W}x{H}/image")
+    assert ctx.set_draw_sub() == sub
 
 
 @pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
-def test_non_finite_colours_match_oracle(ctx, oracle, flags):
+def test_non_finite_colours_match_oracle(ctx, oracle, flags, sub):
     """splats whose colour is +-inf or NaN (f_dc non-finite): the blend keeps a pixel by selects
     when an event does not blend (a batch with a non-finite colour; `rgb * 0` would be NaN), and
     the image still equals the oracle bit for bit"""
@@ -123,7 +133,7 @@ def test_non_finite_colours_match_oracle(ctx, oracle, flags):
     assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), "non-finite colours/image")
 
 
-def test_cull_is_exact_and_frames_deterministic(ctx):
+def test_cull_is_exact_and_frames_deterministic(ctx, sub):
     """the per-block cull never changes a pixel; repeated frames are bit-identical"""
     from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
     raw = bicycle_standin_raw(400_000, seed=3)
@@ -200,22 +210,50 @@ def test_scene_size_limit(ctx):
     assert b"2^27" in N.lib().gs_last_error(ctx.handle)
 
 
-@pytest.mark.parametrize("W,H,view", [(3840, 2160, 0), (1920, 1080, 1), (1920, 1080, 7)])
-def test_full_size_other_configs(ctx, oracle, W, H, view):
-    """the other benchmarked frames at full size, ref mode, bit-exact against the oracle: C4
-    (4K) and C5 views 1 and 7 (pose k = main pose + rotateRight(45 deg * k), what ranks 1 and 7
-    render in the multi-GPU runs)"""
-    from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
-    sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+def full_frame_vs_oracle(sp, oracle, W, H, view, flags=0, sub=0):
+    sp.ctx.set_draw_sub(sub)
     cam = g.main_camera(W, H)
     cam.rotateRight(45.0 * view)
     u = cam.uniforms()
-    r = gpu_frame(sp, u, 0)
-    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0, draw=True)
+    r = gpu_frame(sp, u, flags)
+    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags, draw=True)
     assert [r["V"], r["D"], r["E"]] == [o["V"], o["D"], o["E"]]
     for k in ("keys", "vals", "bins"):
         assert_bits(r[k], o[k], f"{W}x{H} view {view}/{k}")
     assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{W}x{H} view {view}/image")
+    if sub:
+        assert sp.ctx.set_draw_sub() == sub
+    sp.ctx.set_draw_sub(0)
+    return r
+
+
+def test_full_size_c4(ctx, oracle):
+    """C4 (the bicycle-sized scene at 3840x2160), ref mode, bit-exact against the oracle"""
+    from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
+    sp = g.Splats.from_raw(*bicycle_standin_raw(), 3840, 2160, ctx=ctx)
+    full_frame_vs_oracle(sp, oracle, 3840, 2160, 0)
+
+
+@pytest.fixture(scope="module")
+def c5_scene(ctx):
+    from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
+    return g.Splats.from_raw(*bicycle_standin_raw(), 1920, 1080, ctx=ctx)
+
+
+@pytest.mark.parametrize("view", [1, 2, 3, 4, 5, 6, 7])
+def test_c5_views(ctx, oracle, c5_scene, view):
+    """every C5 pose at full size (pose k = main pose + rotateRight(45 deg * k), what rank k renders
+    in the multi-GPU runs; view 0 is C3, test_full_size_properties), ref mode, bit-exact against
+    the oracle.  Views 2-7 are the small-entry frames (0.16-0.96M entries), which blend in 8x8
+    sub-blocks; view 4 also in the other form."""
+    r = full_frame_vs_oracle(c5_scene, oracle, 1920, 1080, view)
+    if view == 4:
+        ctx.set_draw_sub(16)
+        cam = g.main_camera(1920, 1080)
+        cam.rotateRight(45.0 * view)
+        r16 = gpu_frame(c5_scene, cam.uniforms(), 0)
+        assert ctx.set_draw_sub(0) == 16
+        assert np.array_equal(r16["image"], r["image"])
 
 
 @pytest.mark.parametrize("staged", [False, True])
@@ -246,3 +284,17 @@ def test_culled_entries_drawn_as_splat_zero(oracle, staged):
     sp2.render_uniforms(u)
     assert np.array_equal(sp2.texture(), ref2["image"])
     ctx.close()
+
+
+@pytest.mark.parametrize("view", [0, 4])
+def test_small_forms_forced_on_large_frames(ctx, oracle, c5_scene, view):
+    """the small-frame forms on any frame: the 8-launch sort (k_sweep_small) and the 8x8 blend forced
+    on the full C3 frame (10M entries) and the small view 4 -- and both turned off on view 4 -- all
+    bit-exact against the oracle"""
+    try:
+        ctx.set_small_limits(1 << 40, 1 << 40)
+        full_frame_vs_oracle(c5_scene, oracle, 1920, 1080, view, sub=8)
+        ctx.set_small_limits(0, 0)
+        full_frame_vs_oracle(c5_scene, oracle, 1920, 1080, view, sub=16)
+    finally:
+        ctx.set_small_limits(2 << 20, 512 << 10)
