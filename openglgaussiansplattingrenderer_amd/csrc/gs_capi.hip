@@ -255,11 +255,12 @@ int ensure_splats(gs_ctx *ctx, int n) {
     int rc;
     if ((rc = grow(ctx, ctx->L->sd, cap)) || (rc = grow(ctx, ctx->L->cullbox, cap)) ||
         (rc = grow(ctx, ctx->L->rec, cap)) || (rc = grow(ctx, ctx->L->blocksum, nb)) ||
-        (rc = grow(ctx, ctx->L->lb, 2 * (size_t)nb)))
+        (rc = grow(ctx, ctx->L->lb, 2 * (size_t)gs::pre_emit_blocks(cap))))
         return rc;
     // (ordered on the lane's stream with the kernels that use it)
-    GS_HIP(ctx, hipMemsetAsync(ctx->L->lb, 0, 2 * (size_t)nb * sizeof(uint64_t), ctx->L->stream));
-    ctx->L->lb_cap = (uint32_t)nb;
+    const size_t nbe = (size_t)gs::pre_emit_blocks(cap);
+    GS_HIP(ctx, hipMemsetAsync(ctx->L->lb, 0, 2 * nbe * sizeof(uint64_t), ctx->L->stream));
+    ctx->L->lb_cap = (uint32_t)nbe;
     ctx->L->lb_par = 0;
     ctx->L->n_cap = cap;
     return GS_OK;

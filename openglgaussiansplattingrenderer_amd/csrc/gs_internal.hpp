@@ -214,6 +214,7 @@ struct FrameDev {
     float4 *col;         // per-frame colours of GS_FLAG_SH frames (else null)
 };
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
+int pre_emit_blocks(int n);    // workgroups of k_pre_emit (= its look-back status words)
 // start / stop: optional hipEvents recorded on the dispatch packets (stage timing)
 // lazy: the covariance / opacity loads only for the splats inside the NDC square (preprocess_one)
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,

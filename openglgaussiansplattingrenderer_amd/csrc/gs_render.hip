@@ -130,24 +130,54 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_w
 // its computeColorFromSH), for the direction from the camera to the splat; colour =
 // max(SH + 0.5, 0) * 255 so that with f_rest = 0 it is the reference's (0.5 + SH_C0 * f_dc) * 255
 // wherever that is non-negative.  The oracle (ora_sh_colours) evaluates the same op sequence.
-__device__ __forceinline__ float sh_channel(const float *sh, size_t n, size_t i, int c, float x, float y, float z) {
+// one channel from its 16 coefficients k[j] (values in registers)
+__device__ __forceinline__ float sh_channel_k(const float *k, float x, float y, float z) {
     const float SH_C0 = 0.28209479177387814f, SH_C1 = 0.4886025119029199f;
     const float SH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
                             0.5462742152960396f};
     const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
                             -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
-    const float *k = sh + (size_t)(16 * c) * n + i;  // plane 16c + j holds coefficient j of channel c
     float r = SH_C0 * k[0];
-    r = r - SH_C1 * y * k[n] + SH_C1 * z * k[2 * n] - SH_C1 * x * k[3 * n];
+    r = r - SH_C1 * y * k[1] + SH_C1 * z * k[2] - SH_C1 * x * k[3];
     const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-    r = r + SH_C2[0] * xy * k[4 * n] + SH_C2[1] * yz * k[5 * n] + SH_C2[2] * (2.0f * zz - xx - yy) * k[6 * n] +
-        SH_C2[3] * xz * k[7 * n] + SH_C2[4] * (xx - yy) * k[8 * n];
-    r = r + SH_C3[0] * y * (3.0f * xx - yy) * k[9 * n] + SH_C3[1] * xy * z * k[10 * n] +
-        SH_C3[2] * y * (4.0f * zz - xx - yy) * k[11 * n] + SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * k[12 * n] +
-        SH_C3[4] * x * (4.0f * zz - xx - yy) * k[13 * n] + SH_C3[5] * z * (xx - yy) * k[14 * n] +
-        SH_C3[6] * x * (xx - 3.0f * yy) * k[15 * n];
+    r = r + SH_C2[0] * xy * k[4] + SH_C2[1] * yz * k[5] + SH_C2[2] * (2.0f * zz - xx - yy) * k[6] +
+        SH_C2[3] * xz * k[7] + SH_C2[4] * (xx - yy) * k[8];
+    r = r + SH_C3[0] * y * (3.0f * xx - yy) * k[9] + SH_C3[1] * xy * z * k[10] +
+        SH_C3[2] * y * (4.0f * zz - xx - yy) * k[11] + SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * k[12] +
+        SH_C3[4] * x * (4.0f * zz - xx - yy) * k[13] + SH_C3[5] * z * (xx - yy) * k[14] +
+        SH_C3[6] * x * (xx - 3.0f * yy) * k[15];
     r = r + 0.5f;
     return fmaxf(r, 0.0f) * 255.0f;
+}
+__device__ __forceinline__ float sh_channel(const float *sh, size_t n, size_t i, int c, float x, float y, float z) {
+    const float *p = sh + (size_t)(16 * c) * n + i;  // plane 16c + j holds coefficient j of channel c
+    float k[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) k[j] = p[(size_t)j * n];
+    return sh_channel_k(k, x, y, z);
+}
+
+// The SH colours of a frame's splats with entries (GS_FLAG_SH), after k_preprocess (its emission
+// records say which): one splat per lane, all 48 coefficient loads issued before the arithmetic
+// (coalesced planes, ~9 KB in flight per wave) -- in the preprocess they came after its own
+// loads and math, under its register budget, in several round trips per item.
+template <bool PACK>
+__global__ __launch_bounds__(kBlock) void k_sh_colour(PreParams P, SceneDev sc, FrameDev fr) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P.n) return;
+    const bool has = PACK ? (reinterpret_cast<const uint2 *>(fr.rec)[i].y >> 31) != 0 : fr.rec[i].y >= 0;
+    if (!has) return;
+    const size_t n = (size_t)P.n;
+    float k[48];
+#pragma unroll
+    for (int j = 0; j < 48; ++j) k[j] = sc.sh[(size_t)j * n + i];
+    float dx = sc.mx[i] - P.campos[0], dy = sc.my[i] - P.campos[1], dz = sc.mz[i] - P.campos[2];
+    const float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    dx = dx / len;
+    dy = dy / len;
+    dz = dz / len;
+    fr.col[i] = make_float4(sh_channel_k(k, dx, dy, dz), sh_channel_k(k + 16, dx, dy, dz), sh_channel_k(k + 32, dx, dy, dz),
+                            1.0f);
 }
 
 // ------------------------------------------------------------------ preprocess
@@ -644,7 +674,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-template <bool PACK, bool CLEAN, bool LAZY>
+// KP items of 64 splats per wave (KP * 256 splats per workgroup): 1 for the small scenes it runs
+// on (one memory round trip per splat, four times the workgroups of k_preprocess)
+template <bool PACK, bool CLEAN, bool LAZY, int KP>
 __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, FrameDev fr, LookbackDev lb,
                                                      uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                                                      uint32_t cap, uint32_t dup_base, uint32_t *__restrict__ phist,
@@ -652,8 +684,8 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
     // the workgroup's emission records and per-item inclusive duplicate counts stay in LDS between
     // the preprocessing and the emission (in registers they held the kernel to 5 waves per SIMD)
     using Rec = typename std::conditional<PACK, uint2, int4>::type;
-    __shared__ Rec s_rec[kSplatsPerBlock];
-    __shared__ uint16_t s_incl[kBlock / 64][kPer][64];  // (<= 64 * 256 per item)
+    __shared__ Rec s_rec[KP * kBlock];
+    __shared__ uint16_t s_incl[kBlock / 64][KP][64];  // (<= 64 * 256 per item)
     __shared__ uint2 s_tot[kBlock / 64];
     __shared__ uint2 s_off;
     const uint32_t blk = blockIdx.x;
@@ -661,11 +693,11 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
     // frame before, is complete)
     for (uint32_t j = blk * kBlock + threadIdx.x; j < lb.cap_blocks; j += nblocks * kBlock) lb.st_next[j] = 0ull;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const int wbase = (int)blk * kSplatsPerBlock + wid * (kPer * 64);
-    Rec *wrec = s_rec + wid * (kPer * 64);
+    const int wbase = (int)blk * (KP * kBlock) + wid * (KP * 64);
+    Rec *wrec = s_rec + wid * (KP * 64);
     uint32_t tot_m = 0, tot_d = 0;
 #pragma unroll 1
-    for (int j = 0; j < kPer; ++j) {
+    for (int j = 0; j < KP; ++j) {
         const int i = wbase + j * 64 + lane;
         const int4 rc = preprocess_one<CLEAN, LAZY>(P, sc, fr, i, i < P.n);
         if constexpr (PACK)
@@ -742,7 +774,7 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
     uint32_t run_m = s_off.x + wm, run_d = s_off.y + wd;
     // the emission (k_emit's, from the records in LDS; duplicates at dup_base)
 #pragma unroll 1
-    for (int it = 0; it < kPer; ++it) {
+    for (int it = 0; it < KP; ++it) {
         const Rec raw = wrec[it * 64 + lane];
         int4 rc;
         if constexpr (PACK) rc = unpack_rec(raw);
@@ -1107,6 +1139,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_refresh = 0;
     unsigned long long st_a192 = 0, st_a128 = 0, st_a64 = 0, st_dev = 0;  // dense steps by active pixels
+#ifndef GS_STATS_NEV
+#define GS_STATS_NEV 0
+#endif
+#if GS_STATS_NEV
+    uint32_t st_pn = 0;
+    uint64_t st_p0 = 0, st_p1 = 0, st_p2 = 0, st_p3 = 0;
+#endif
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
     const int jmax = max(end - 1, 0);
@@ -1322,10 +1361,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 st_ev64 += active <= 64 ? nev : 0;
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
+#if GS_STATS_NEV  // (experiment) dense steps by event count, and greedy pairs of consecutive steps
+                  // whose events fit one pass on distinct pixels
+                st_a192 += (nev > 0 && nev <= 16) ? 1 : 0;
+                st_a128 += (nev > 16 && nev <= 32) ? 1 : 0;
+                st_a64 += (nev > 32 && nev <= 48) ? 1 : 0;
+                if (nev) {
+                    const bool merge = st_pn && st_pn + nev <= 64 &&
+                                       !((st_p0 & b0) | (st_p1 & b1) | (st_p2 & b2) | (st_p3 & b3));
+                    st_dev += merge ? 1 : 0;
+                    st_pn = merge ? 0 : nev;
+                    st_p0 = b0;
+                    st_p1 = b1;
+                    st_p2 = b2;
+                    st_p3 = b3;
+                }
+#else
                 st_a192 += active > 192 ? 1 : 0;
                 st_a128 += (active > 128 && active <= 192) ? 1 : 0;
                 st_a64 += (active > 64 && active <= 128) ? 1 : 0;
                 st_dev += nev;
+#endif
             }
             if (nev != 0) {  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
@@ -1554,15 +1610,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
 }  // namespace
 
 int preprocess_blocks(int n) { return (n + kSplatsPerBlock - 1) / kSplatsPerBlock; }
+int pre_emit_blocks(int n) { return (n + kBlock - 1) / kBlock; }
 
 // Stage timing rides on the dispatch packets (hipExtLaunchKernelGGL start / stop events): a
 // separate hipEventRecord costs an idle gap of several microseconds on the stream.
 bool rec_packed(const PreParams &P) { return P.clean || (P.W >= 16 && P.H >= 16); }
 
-void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
+void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
                        bool lazy) {
-    const int nb = preprocess_blocks(P.n);
+    const int nb = preprocess_blocks(P0.n);
     if (nb <= 0) return;
+    PreParams P = P0;
+    P.sh = 0;  // GS_FLAG_SH: the colours in a kernel of their own (k_sh_colour), after the records
 #define GS_PRE(PK, CL, LZ) \
     hipExtLaunchKernelGGL((k_preprocess<PK, CL, LZ>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr)
     if (P.clean) {  // (clean mode always packs its records)
@@ -1575,6 +1634,11 @@ void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, co
         GS_PRE(false, false, false);
     }
 #undef GS_PRE
+    if (P0.sh) {
+        const dim3 g((P0.n + kBlock - 1) / kBlock);
+        if (P.clean || rec_packed(P)) hipLaunchKernelGGL(k_sh_colour<true>, g, dim3(kBlock), 0, s, P0, sc, fr);
+        else hipLaunchKernelGGL(k_sh_colour<false>, g, dim3(kBlock), 0, s, P0, sc, fr);
+    }
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
@@ -1591,14 +1655,15 @@ void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t
 void launch_pre_emit(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const LookbackDev &lb,
                      bool lazy, uint32_t *keys, uint32_t *vals, uint32_t cap, uint32_t *prefix_hist, hipEvent_t start,
                      hipEvent_t stop) {
-    const uint32_t nb = (uint32_t)preprocess_blocks(P.n);
+    constexpr int KP = 1;
+    const uint32_t nb = (uint32_t)pre_emit_blocks(P.n);
     if (nb == 0) {  // no splats: no entries
         hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, 0);
         return;
     }
     const uint32_t dup_base = (uint32_t)P.n;
 #define GS_PE(PK, CL, LZ)                                                                                          \
-    hipExtLaunchKernelGGL((k_pre_emit<PK, CL, LZ>), dim3(nb), dim3(kBlock), 0, s, start, stop, 0, P, sc, fr, lb, keys, \
+    hipExtLaunchKernelGGL((k_pre_emit<PK, CL, LZ, KP>), dim3(nb), dim3(kBlock), 0, s, start, stop, 0, P, sc, fr, lb, keys, \
                           vals, cap, dup_base, prefix_hist, nb)
     const bool packed = rec_packed(P);
     if (P.clean) {

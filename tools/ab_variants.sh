@@ -12,7 +12,7 @@ for round in 1 2; do
     timeout -k 10 200 python bench.py --no-cpu-baseline --no-sort-bench > gpurun_out/ab_${v}_$round.json 2> gpurun_out/ab.err || { cp /tmp/libgsplat_hip.orig.so $L/libgsplat_hip.so; exit 1; }
     python3 -c "
 import json; d=json.load(open('gpurun_out/ab_${v}_$round.json')); fr=d['frame']
-print('$v r$round fps %.1f' % d['value'], 'serial', fr['serial_ms_per_frame'], 'stages', fr['stage_ms'], 'draw1', d['roofline']['one_frame']['avg_launch_ms'])"
+print('$v r$round fps %.1f' % d['value'], 'serial', fr['serial_ms_per_frame'], 'stages', fr['stage_ms'], 'draw1', d['roofline']['avg_launch_ms'])"
   done
 done
 cp /tmp/libgsplat_hip.orig.so $L/libgsplat_hip.so

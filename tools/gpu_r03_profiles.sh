@@ -4,6 +4,8 @@
 # traced too.  Outputs in gpurun_out/prof_r03/; the summaries are copied into profiles/r03/.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
+cd $R && timeout -k 10 900 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread tests > gpurun_out/prof_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 gpurun_out/prof_tests.log; exit 1; }
+tail -1 gpurun_out/prof_tests.log
 OUT=$R/gpurun_out/prof_r03
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
@@ -28,5 +30,6 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/trace_v4 -o run --out
     python3 $R/bench.py --view 4 --no-cpu-baseline --no-sort-bench > $OUT/v4_under_trace.json 2> $OUT/v4.err || { echo V4_FAIL; exit 1; }
 python3 $R/tools/trace_passes.py $OUT/trace_v4/run_kernel_trace.csv 50 10 100 > $OUT/v4_trace_by_pass.txt
 cd $R
+timeout -k 10 200 python3 bench.py --sh --no-cpu-baseline --no-sort-bench > $OUT/sh.json 2> $OUT/sh.err || { echo SH_FAIL; exit 1; }
 timeout -k 10 300 python3 bench.py > $OUT/bench_latest.json 2> $OUT/bench.err || { echo BENCH_FAIL; exit 1; }
 echo done

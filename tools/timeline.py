@@ -12,7 +12,8 @@ from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw  # no
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 flags = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-W, H = {"c2": (512, 512), "c3": (1920, 1080)}.get(cfg, (3840, 2160))
+view = int(cfg[1:]) if cfg.startswith("v") else 0  # vK: C5 pose K at 1080p
+W, H = {"c2": (512, 512), "c3": (1920, 1080)}.get(cfg, (1920, 1080) if view or cfg == "v0" else (3840, 2160))
 ctx = g.Context(0)
 if cfg == "c2":
     from openglgaussiansplattingrenderer_amd.scenes import c2_scene
@@ -20,7 +21,9 @@ if cfg == "c2":
     sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
 else:
     sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
-u = g.main_camera(W, H).uniforms()
+cam = g.main_camera(W, H)
+cam.rotateRight(45.0 * view)
+u = cam.uniforms()
 sp.flags = flags | g.GS_FLAG_DRAW_STATS
 for _ in range(3):
     sp.render_uniforms(u)
