@@ -216,7 +216,8 @@ struct FrameDev {
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
 int pre_emit_blocks(int n);    // workgroups of k_pre_emit (= its look-back status words)
 // start / stop: optional hipEvents recorded on the dispatch packets (stage timing)
-// lazy: the covariance / opacity loads only for the splats inside the NDC square (preprocess_one)
+// lazy (most splats culled last frame): the queued form, k_preprocess_q -- the bulk of the
+// preprocess, and the covariance / opacity loads, for the splats inside the NDC square only
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
                        bool lazy = false);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);

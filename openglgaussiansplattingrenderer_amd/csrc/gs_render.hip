@@ -223,6 +223,43 @@ __device__ __forceinline__ uint2 pack_box(const float4 &b) {
 // the NDC cull, one round trip later -- for frames where most splats are culled (the small C5
 // views: ~97 % culled, a 64-byte line of a plane then mostly holds culled splats only);
 // otherwise all ten planes are loaded in one round trip.
+// :77-89 the projection and the NDC cull: (p0, p1, p2) and whether x / y lie inside [-1, 1]
+__device__ __forceinline__ bool project_ndc(const PreParams &P, float mx, float my, float mz, float &p0, float &p1,
+                                            float &p2) {
+    p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
+    p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
+    p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
+    const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
+    const float w = fmaxf(p3, 0.0001f);
+    p0 = p0 / w;
+    p1 = p1 / w;
+    p2 = p2 / w;
+    return !(p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f);
+}
+
+// splat 0 without entries: the record its culled entries draw (preprocess.glsl:80-88 splatKeys
+// = 0, reached by a Q10 over-read; k_draw) -- means2D, conic and opacity 0 (never blends:
+// threshold +inf, empty box)
+__device__ __forceinline__ void write_culled_splat0(const FrameDev &fr) {
+    const float inf = __builtin_inff();
+    fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
+}
+
+template <bool CLEAN, bool SH = true>
+__device__ __forceinline__ int4 preprocess_rest(const PreParams &P, const SceneDev &sc, const FrameDev &fr, int i,
+                                                float mx, float my, float mz, float p0, float p1, float p2, bool vis,
+                                                float c0, float c1, float c2, float c3, float c4, float c5, float opac);
+
+// One splat of preprocess.glsl:64-190: its blend record, cull box and (GS_FLAG_SH) colour
+// written when it has entries, and its emission record returned: (z01 bits, tileX, tileY, rect)
+// or (0, -1, -1, 0) without entries (culled, det == 0, or i out of range).
+// CLEAN: clean mode (P.clean) as a template parameter -- a uniform flag's alternatives were
+// if-converted into selects that every splat evaluated.
+// LAZY: the covariance and opacity (28 of the 40 bytes) are loaded only for the lanes that pass
+// the NDC cull, one round trip later -- for frames where most splats are culled (the small C5
+// views: ~97 % culled, a 64-byte line of a plane then mostly holds culled splats only);
+// otherwise all ten planes are loaded in one round trip.
 template <bool CLEAN, bool LAZY>
 __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDev &sc, const FrameDev &fr, int i,
                                                bool valid) {
@@ -239,17 +276,8 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
     // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
     // all ten plane loads issue up front and no exec-mask bookkeeping runs).  Culled lanes
     // compute garbage (inf / NaN) that is never used.
-    // :77-78
-    float p0 = m4v_row(P.vp, 0, mx, my, mz, 1.0f);
-    float p1 = m4v_row(P.vp, 1, mx, my, mz, 1.0f);
-    float p2 = m4v_row(P.vp, 2, mx, my, mz, 1.0f);
-    const float p3 = m4v_row(P.vp, 3, mx, my, mz, 1.0f);
-    const float w = fmaxf(p3, 0.0001f);
-    p0 = p0 / w;
-    p1 = p1 / w;
-    p2 = p2 / w;
-    // :80-89 cull: NDC x/y only
-    bool vis = !(p0 < -1.0f || p0 > 1.0f || p1 < -1.0f || p1 > 1.0f);
+    float p0, p1, p2;
+    const bool vis = project_ndc(P, mx, my, mz, p0, p1, p2);
     if (LAZY) {
         c0 = c1 = c2 = c3 = c4 = c5 = opac = 0.0f;
         if (vis) {
@@ -258,6 +286,16 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
             opac = sc.opacity[i];
         }
     }
+    return preprocess_rest<CLEAN>(P, sc, fr, i, mx, my, mz, p0, p1, p2, vis, c0, c1, c2, c3, c4, c5, opac);
+}
+
+// preprocess.glsl:91-190 after the NDC cull (vis: the splat passed it).  SH: the GS_FLAG_SH
+// colour here (k_pre_emit); the other kernels leave it to k_sh_colour.
+template <bool CLEAN, bool SH>
+__device__ __forceinline__ int4 preprocess_rest(const PreParams &P, const SceneDev &sc, const FrameDev &fr, int i,
+                                                float mx, float my, float mz, float p0, float p1, float p2, bool vis,
+                                                float c0, float c1, float c2, float c3, float c4, float c5, float opac) {
+    const size_t n = (size_t)P.n;
     // :91-94
     float sx = (p0 + 1.0f) * 0.5f, sy = (p1 + 1.0f) * 0.5f;
     const float sz = (p2 + 1.0f) * 0.5f;
@@ -345,7 +383,7 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
     if (rc.y >= 0) {
         fr.sd[i] = SplatDraw{m2.x, m2.y, co.x, co.y, co.z, co.w};
         fr.cullbox[i] = pack_box(box);
-        if (P.sh) {  // GS_FLAG_SH: this frame's colour
+        if (SH && P.sh) {  // GS_FLAG_SH: this frame's colour
             float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
             const float len = sqrtf(dx * dx + dy * dy + dz * dz);
             dx = dx / len;
@@ -355,8 +393,7 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
                                     sh_channel(sc.sh, n, i, 2, dx, dy, dz), 1.0f);
         }
     } else if (i == 0) {  // splat 0 culled: the record its culled entries draw
-        fr.sd[0] = SplatDraw{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // threshold +inf
-        fr.cullbox[0] = pack_box(make_float4(inf, -inf, inf, -inf));
+        write_culled_splat0(fr);
     }
     return rc;
 }
@@ -397,6 +434,122 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         tot_dup = tot >> 11;
     }
     if (threadIdx.x == 0) fr.blocksum[blockIdx.x] = make_uint2(tot_main, tot_dup);
+}
+
+// The same records with the NDC cull compacted out (QUEUE form).  kQWaves waves share a
+// workgroup's kSplatsPerBlock splats (the block sums keep k_emit's granularity), each wave a
+// contiguous run of kQItems * 64.  For each 64 of them a wave runs the projection (project_ndc),
+// writes the culled splats' records at once and pushes the survivors -- (index, p0, p1, p2) --
+// into a queue held in registers, one entry per lane, by a forward permute (ds_permute: the
+// survivors to the next free queue lanes, the others to the remaining lanes, a permutation, so
+// no two lanes collide).  Whenever 64 entries are queued they become the pending chunk: their
+// ten plane loads are issued at once and every lane runs the rest of the preprocess
+// (preprocess_rest) on one of them one projection step later, so the gathers are in flight
+// behind that step's arithmetic (as the next projection's three loads are behind this one's);
+// the remainder is flushed at the end.  The straight-line form (k_preprocess) computes the whole
+// preprocess in every lane of a wave that has any survivor -- nearly every wave, so the culled
+// splats' share of its arithmetic was spent for nothing (24 % at C3; ~97 % in the small C5
+// views, where this also leaves their covariance and opacity unread).
+#ifndef GS_QWAVES
+#define GS_QWAVES 2
+#endif
+constexpr int kQWaves = GS_QWAVES;
+constexpr int kQItems = kSplatsPerBlock / (64 * kQWaves);
+template <bool PACK, bool CLEAN>
+__global__ __launch_bounds__(64 * kQWaves) void k_preprocess_q(PreParams P, SceneDev sc, FrameDev fr) {
+    __shared__ uint32_t s_sum[kQWaves];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const size_t n = (size_t)P.n;
+    const int base = blockIdx.x * kSplatsPerBlock + wid * (kQItems * 64);
+    uint32_t n_main = 0, n_dup = 0;
+    // queue: entries [0, qn) in lanes of qa (the first 64) and qb (the overflow)
+    int qa_i = 0, qb_i = 0;
+    float qa0 = 0.0f, qa1 = 0.0f, qa2 = 0.0f, qb0 = 0.0f, qb1 = 0.0f, qb2 = 0.0f;
+    int qn = 0;
+    // the pending chunk: lanes [0, pend_n) hold a survivor and its loaded planes
+    int pend_n = 0, pi = 0;
+    float pp0 = 0.0f, pp1 = 0.0f, pp2 = 0.0f, pmx = 0.0f, pmy = 0.0f, pmz = 0.0f;
+    float pc0 = 0.0f, pc1 = 0.0f, pc2 = 0.0f, pc3 = 0.0f, pc4 = 0.0f, pc5 = 0.0f, pop = 0.0f;
+    auto write_rec = [&](int i, const int4 &rc) {
+        if (PACK)
+            reinterpret_cast<uint2 *>(fr.rec)[i] = make_uint2((uint32_t)rc.x, rc.y >= 0 ? pack_rec(rc.y, rc.z, (uint32_t)rc.w) : 0u);
+        else
+            fr.rec[i] = rc;
+    };
+    // the next projection step's means, loaded one step ahead
+    float nmx = 0.0f, nmy = 0.0f, nmz = 0.0f;
+    if (base + lane < P.n) nmx = sc.mx[base + lane], nmy = sc.my[base + lane], nmz = sc.mz[base + lane];
+#pragma unroll 1
+    for (int it = 0; it <= kQItems + 1; ++it) {
+        if (it < kQItems) {  // projection step
+            const int i = base + it * 64 + lane;
+            const bool valid = i < P.n;
+            const float mx = nmx, my = nmy, mz = nmz;
+            if (it + 1 < kQItems && i + 64 < P.n) nmx = sc.mx[i + 64], nmy = sc.my[i + 64], nmz = sc.mz[i + 64];
+            float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+            bool vis = false;
+            if (valid) {
+                vis = project_ndc(P, mx, my, mz, p0, p1, p2);
+                if (!vis) {
+                    write_rec(i, make_int4(0, -1, -1, 0));
+                    if (i == 0) write_culled_splat0(fr);
+                }
+            }
+            const uint64_t m = __ballot(vis);
+            const int cnt = __popcll(m);
+            if (cnt) {
+                // survivors to queue lanes qn, qn+1, ... (mod 64), the others after them
+                const int r_in = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                const int dst = (vis ? qn + r_in : qn + cnt + (lane - r_in)) & 63;
+                const int addr = dst << 2;
+                const int gi = __builtin_amdgcn_ds_permute(addr, i);
+                const float g0 = __int_as_float(__builtin_amdgcn_ds_permute(addr, __float_as_int(p0)));
+                const float g1 = __int_as_float(__builtin_amdgcn_ds_permute(addr, __float_as_int(p1)));
+                const float g2 = __int_as_float(__builtin_amdgcn_ds_permute(addr, __float_as_int(p2)));
+                const bool fresh = ((lane - qn) & 63) < cnt;
+                if (fresh && lane >= qn) {
+                    qa_i = gi, qa0 = g0, qa1 = g1, qa2 = g2;
+                } else if (fresh) {
+                    qb_i = gi, qb0 = g0, qb1 = g1, qb2 = g2;
+                }
+                qn += cnt;
+            }
+        }
+        if (pend_n > 0) {  // the pending chunk, its planes loaded one step ago
+            if (lane < pend_n) {
+                const int4 rc = preprocess_rest<CLEAN, false>(P, sc, fr, pi, pmx, pmy, pmz, pp0, pp1, pp2, true, pc0, pc1, pc2, pc3,
+                                                       pc4, pc5, pop);
+                write_rec(pi, rc);
+                n_main += rc.y >= 0 ? 1u : 0u;
+                n_dup += rec_dups(rc);
+            }
+            pend_n = 0;
+        }
+        if (qn >= 64 || (it == kQItems && qn > 0)) {  // a full queue (or the rest) becomes pending
+            pend_n = qn < 64 ? qn : 64;
+            pi = qa_i, pp0 = qa0, pp1 = qa1, pp2 = qa2;
+            if (lane < pend_n) {
+                pmx = sc.mx[pi], pmy = sc.my[pi], pmz = sc.mz[pi];
+                pc0 = sc.cov[pi], pc1 = sc.cov[n + pi], pc2 = sc.cov[2 * n + pi];
+                pc3 = sc.cov[3 * n + pi], pc4 = sc.cov[4 * n + pi], pc5 = sc.cov[5 * n + pi];
+                pop = sc.opacity[pi];
+            }
+            qa_i = qb_i, qa0 = qb0, qa1 = qb1, qa2 = qb2;
+            qn -= pend_n;
+        }
+    }
+    // block sums of (main, dup): mains in the low 11 bits (<= 1024), duplicates above (see k_preprocess)
+    uint32_t v = n_main | (n_dup << 11);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s_sum[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kQWaves; ++w) t += s_sum[w];
+        fr.blocksum[blockIdx.x] = make_uint2(t & 0x7ffu, t >> 11);
+    }
 }
 
 // exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1].
@@ -1622,16 +1775,21 @@ void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, c
     if (nb <= 0) return;
     PreParams P = P0;
     P.sh = 0;  // GS_FLAG_SH: the colours in a kernel of their own (k_sh_colour), after the records
-#define GS_PRE(PK, CL, LZ) \
-    hipExtLaunchKernelGGL((k_preprocess<PK, CL, LZ>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr)
+    // most splats culled last frame (lazy): the queued form, which runs the bulk of the
+    // preprocess on the NDC survivors only; else the straight-line form (at C3's 76 % survivors
+    // the queue's bookkeeping and gathers cost more than the culled lanes' arithmetic it saves:
+    // preprocess 0.110 -> 0.125 ms; view 4 (~3 % survivors) 0.075 -> 0.036 ms)
+#define GS_PRE(PK, CL)                                                                                                      \
+    if (lazy)                                                                                                               \
+        hipExtLaunchKernelGGL((k_preprocess_q<PK, CL>), dim3(nb), dim3(64 * kQWaves), 0, s, start, nullptr, 0, P, sc, fr); \
+    else                                                                                                                    \
+        hipExtLaunchKernelGGL((k_preprocess<PK, CL, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr)
     if (P.clean) {  // (clean mode always packs its records)
-        if (lazy) GS_PRE(true, true, true);
-        else GS_PRE(true, true, false);
+        GS_PRE(true, true);
     } else if (rec_packed(P)) {
-        if (lazy) GS_PRE(true, false, true);
-        else GS_PRE(true, false, false);
+        GS_PRE(true, false);
     } else {
-        GS_PRE(false, false, false);
+        GS_PRE(false, false);
     }
 #undef GS_PRE
     if (P0.sh) {

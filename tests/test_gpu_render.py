@@ -112,6 +112,30 @@ def test_non_multiple_of_16_resolutions(ctx, oracle, W, H, n, flags, sub):
     assert ctx.set_draw_sub() == sub
 
 
+@pytest.mark.parametrize("W,H,turn,flags", [(1920, 1080, 60, 0), (1920, 1080, 60, g.GS_FLAG_CLEAN),
+                                             (12, 40, 30, 0)])  # 12 px: 16-byte records
+def test_queued_preprocess_on_mostly_culled_frames(oracle, W, H, turn, flags):
+    """a frame that follows one with fewer than half its splats inside the NDC square runs the
+    queued preprocess (k_preprocess_q: the bulk of the preprocess on the NDC survivors only), the
+    first frame of a context the straight-line one: both bit-exact against the oracle (100k
+    splats, above the fused preprocess + emission's size)"""
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene(100_000, seed=9)  # > 64 preprocess blocks: not the fused form
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    cam = g.main_camera(W, H)
+    cam.rotateRight(float(turn))
+    u = cam.uniforms()
+    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags)
+    assert 0 < o["V"] * 2 < sp.numSplats  # the second frame takes the queued form
+    for frame in ("straight", "queued"):
+        r = gpu_frame(sp, u, flags)
+        assert [r["V"], r["D"], r["E"]] == [o["V"], o["D"], o["E"]], frame
+        for k in ("means2d", "conics", "keys", "vals", "bins"):
+            assert_bits(r[k], o[k], f"{frame}/{k}")
+        assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{frame}/image")
+
+
 @pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
 def test_non_finite_colours_match_oracle(ctx, oracle, flags, sub):
     """splats whose colour is +-inf or NaN (f_dc non-finite): the blend keeps a pixel by selects
