@@ -119,6 +119,10 @@ int gs_ctx_set_draw_sub(gs_ctx *ctx, int sub, int *current);
  * blend in 8x8 sub-blocks when gs_ctx_set_draw_sub is 0 (default 2^21), and below sort_entries
  * sort in 8 launches instead of 12 (default 2^19).  A negative value leaves a limit. */
 int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entries);
+/* The small sort's form: 1 (default) = by tile, then each tile's list (3 launches: a stable
+ * scatter by int(key), then LSD passes per tile in LDS); 0 = four 8-bit passes (8 launches);
+ * -1 leaves it.  Returns the form now set (or a negative GS_ERR_*).  Same result either way. */
+int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on);
 /* prefix-sort counters: [0] frames prefix-sorted, [1] of them rendered again (a blend reached
  * an unsorted position), [2] entries kept by the newest retired prefix-sorted frame, [3] its
  * entry count; reset != 0 clears [0] and [1] */

@@ -115,6 +115,7 @@ SIGNATURES = {
     "gs_ctx_set_sort_prefix": (_i, [_vp, _i, ctypes.POINTER(_i)]),
     "gs_ctx_set_draw_sub": (_i, [_vp, _i, ctypes.POINTER(_i)]),
     "gs_ctx_set_small_limits": (_i, [_vp, ctypes.c_int64, ctypes.c_int64]),
+    "gs_ctx_set_bucket_sort": (_i, [_vp, _i]),
     "gs_prefix_stats": (_i, [_vp, _vp, _i]),
     "gs_malloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
     "gs_free": (_i, [_vp, _vp]),

@@ -158,6 +158,7 @@ struct gs_ctx {
     // seen) blend in 8x8 sub-blocks (draw_sub 0) and sort in 8 launches (k_sweep_small)
     int64_t small_draw_entries = kSmallDrawEntries;
     int64_t small_sort_entries = kSmallSortEntries;
+    bool bucket_sort = true;  // the small sort form: by tile, then per tile (3 launches); else 8 launches
 };
 
 struct gs_scene {
@@ -970,7 +971,8 @@ int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins =
     small = small && with_bins && !pre;
     const bool keys_out = small || (!pre && (!with_bins || ctx->n > (1 << 24)));
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
-                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre, dup_base, small))
+                                fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre, dup_base, small,
+                                small && ctx->bucket_sort))
         return set_error(ctx, rc, ctx->err);
     ctx->L->keys_sorted = keys_out;
     ctx->L->vals_partial = pre != nullptr;
@@ -1327,6 +1329,12 @@ int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entr
     if (draw_entries >= 0) ctx->small_draw_entries = draw_entries;
     if (sort_entries >= 0) ctx->small_sort_entries = sort_entries;
     return GS_OK;
+}
+
+int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (on >= 0) ctx->bucket_sort = on != 0;
+    return ctx->bucket_sort ? 1 : 0;
 }
 
 int gs_ctx_set_draw_sub(gs_ctx *ctx, int sub, int *current) {

@@ -153,6 +153,7 @@ struct SortScratch {
     uint32_t *hist = nullptr;      // [256][nb]
     size_t hist_cap = 0;           // elements
     uint32_t *row_total = nullptr; // [256], then [16][256] tile counts (zero between sorts)
+    uint32_t *bkt = nullptr;       // [2][256]: the bucket form's bucket bases and counts
 };
 
 // Stable sort of (key, value) pairs: n elements, or -- when dev_count is given -- min(n,
@@ -171,9 +172,11 @@ struct SortScratch {
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
                uint32_t *bins = nullptr, bool keys_out = true, const PrefixDev *pre = nullptr,
-               int64_t dup_base = -1, bool small = false);
+               int64_t dup_base = -1, bool small = false, bool bucket = false);
 // small (not with pre): the form for few entries -- 8 launches instead of 12 (k_sweep_small);
 // keys and values come out sorted.  Any n is sorted correctly; it pays off while n is small.
+// bucket (with small): 3 launches -- a stable scatter by tile (bucket_of) and k_bucket_sort's
+// per-bucket LSD passes in LDS (a bucket over 4096 keys through global memory, still exact).
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small = false);
 void sort_free(SortScratch &sc);
 // argsort helper: keys_out[i] = bits(keys[order[i]]), vals_out[i] = order[i]

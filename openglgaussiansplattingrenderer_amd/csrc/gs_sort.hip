@@ -153,7 +153,20 @@ __device__ __forceinline__ uint32_t split_at(uint32_t idx, uint32_t v0, uint32_t
     return idx >= v0 ? idx + gap : idx;
 }
 
-template <int W, bool TILES, bool PREFIX = false>
+// The bucket sort's first digit (BKT): the key's tile, int(key) as a float, for keys below 255.0;
+// 255 for every key from 255.0's bits on (tile 255's keys, 1e6, +inf, NaN and the negative
+// floats, which sort after them as unsigned words).  Monotone in the unsigned key, so a stable
+// scatter by it followed by a stable sort of each bucket is the stable sort of the keys.
+constexpr uint32_t kBits255 = 0x437f0000u;  // 255.0f
+__device__ __forceinline__ uint32_t bucket_of(uint32_t key) {
+    return key >= kBits255 ? 255u : (uint32_t)f2i(__uint_as_float(key));
+}
+template <bool BKT>
+__device__ __forceinline__ uint32_t digit_of(uint32_t key, int shift) {
+    return BKT ? bucket_of(key) : (key >> shift) & 0xffu;
+}
+
+template <int W, bool TILES, bool PREFIX = false, bool BKT = false>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
@@ -218,7 +231,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
                 if (keep) atomicAdd(&s_sel[c * kRep + rep], 1u);
                 low += kk[k] < kKey1Bits ? 1u : 0u;
             }
-            if (keep) atomicAdd(&s_cnt[((kk[k] >> shift) & 0xffu) * kRep + rep], 1u);
+            if (keep) atomicAdd(&s_cnt[digit_of<BKT>(kk[k], shift) * kRep + rep], 1u);
             if (TILES) {  // the frame's tile counts ride on the first pass
                 const uint32_t t = (uint32_t)f2i(__uint_as_float(kk[k]));
                 if (t < (uint32_t)kRadix) atomicAdd(&s_tiles[t * kRep + rep], 1u);
@@ -650,13 +663,16 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
 // few digits put ~800 cross-XCD atomics on each counter, 0.45 ms for the 51k-entry C2 sort.)
 // Any entry count is sorted correctly; the host picks this form for frames whose previous count
 // was small (kSmallSortEntries).  Tiles of 4096 keys (4 waves).
+// BKT: the bucket sort's first pass (digit = bucket_of(key)); the workgroup of tile 0 also writes
+// each bucket's (base, count) to bkt[d], bkt[256 + d] for k_bucket_sort.
+template <bool BKT>
 __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t *__restrict__ kin,
                                                                const uint32_t *__restrict__ vin,
                                                                uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                                uint32_t n_max, const uint32_t *__restrict__ cnt,
                                                                int shift, const uint32_t *__restrict__ hist, uint32_t nb,
                                                                uint32_t dup_base, uint32_t *__restrict__ tile_counts,
-                                                               uint32_t *__restrict__ bins) {
+                                                               uint32_t *__restrict__ bins, uint32_t *__restrict__ bkt) {
     constexpr int kThreads = kWaveSmall * 64, kTile = kThreads * kItems, kWaves = kWaveSmall;
     static_assert(kThreads == kRadix, "one thread per digit");
     __shared__ uint32_t s_w[4];
@@ -719,7 +735,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const bool valid = base + k * 64 < n;
-        const uint32_t dg = (kk[k] >> shift) & 0xffu;
+        const uint32_t dg = digit_of<BKT>(kk[k], shift);
         const uint64_t m = match_digit(dg, __ballot(valid));
         rank[k] = count_below(m);
         lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
@@ -728,7 +744,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         const bool valid = base + k * 64 < n;
-        if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
+        if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][digit_of<BKT>(kk[k], shift)], old[k]);
     }
 #pragma unroll
     for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
@@ -745,12 +761,16 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
         const uint32_t gdig = block_excl_scan<kWaves>(total, s_wave);  // digit base, whole array
         s_start[d] = start;
         s_gbase[d] = (int32_t)(gdig + before) - (int32_t)start;
+        if (BKT && tile == 0) {
+            bkt[d] = gdig;
+            bkt[kRadix + d] = total;
+        }
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
         if (base + k * 64 < n) {
-            const uint32_t dg = (kk[k] >> shift) & 0xffu;
+            const uint32_t dg = digit_of<BKT>(kk[k], shift);
             const uint32_t pos = s_start[dg] + s_cnt[wid][dg] + rank[k];
             s_keys[pos] = kk[k];
             s_vals[pos] = vv[k];
@@ -760,10 +780,189 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
-        const uint32_t o = (uint32_t)(s_gbase[(key >> shift) & 0xffu] + (int32_t)i);
+        const uint32_t o = (uint32_t)(s_gbase[digit_of<BKT>(key, shift)] + (int32_t)i);
         kout[o] = key;
         vout[o] = s_vals[i];
     }
+}
+
+// Stable ranks of one tile of up to 4096 keys held as k_sweep_small holds them (4 waves: wave w,
+// item k, lane l is position w*1024 + k*64 + l; valid below tn): ps[k] = the item's place in the
+// tile's order by digit (key >> shift) & 0xff; s_tdig[d] = the tile's count of digit d, and
+// s_start[d] its first place.  Starts and ends with a barrier.
+__device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t tn, int shift, uint32_t (&ps)[kItems],
+                                          uint32_t (*s_cnt)[kRadix], uint32_t *s_start, uint32_t *s_wave,
+                                          uint32_t *s_tdig) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
+    __syncthreads();  // the previous use of the scratch is done
+#pragma unroll
+    for (int w = 0; w < kWaveSmall; ++w) s_cnt[w][d] = 0;
+    __syncthreads();
+    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
+    uint32_t rank[kItems], lead[kItems], old[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const bool valid = base + k * 64 < tn;
+        const uint64_t m = match_digit((kk[k] >> shift) & 0xffu, __ballot(valid));
+        rank[k] = count_below(m);
+        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
+        old[k] = valid ? (uint32_t)__popcll(m) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const bool valid = base + k * 64 < tn;
+        if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    __syncthreads();
+    uint32_t tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaveSmall; ++w) {
+        const uint32_t c = s_cnt[w][d];
+        s_cnt[w][d] = tot;
+        tot += c;
+    }
+    s_tdig[d] = tot;
+    s_start[d] = block_excl_scan<kWaveSmall>(tot, s_wave);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t dg = (kk[k] >> shift) & 0xffu;
+        ps[k] = s_start[dg] + s_cnt[wid][dg] + rank[k];
+    }
+    __syncthreads();
+}
+
+// The bucket sort's second kernel: bucket b = [bkt[b], + bkt[256 + b]) of (kin, vin), in input
+// order within the bucket (k_sweep_small<true>), stably sorted by key into the same positions
+// of (kout, vout).  The keys of a bucket agree above the highest bit where its smallest and
+// largest differ, so LSD passes over the bits below it (8 per pass: tile 0's depths up to 4,
+// a tile >= 128's keys 2) order it completely.  Buckets of <= 4096 keys sort in registers and
+// LDS; longer ones (rare: a tile list that long in a frame this small) take the same passes
+// through global memory in 4096-key tiles, ping-ponging between the two arrays' bucket ranges.
+__global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__restrict__ kin, uint32_t *__restrict__ vin,
+                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                               const uint32_t *__restrict__ bkt) {
+    static_assert(kWaveSmall * 64 == kRadix, "one thread per digit");
+    constexpr uint32_t kTile = kTileSmall;
+    __shared__ uint32_t s_k[kTile], s_v[kTile];
+    __shared__ uint32_t s_cnt[kWaveSmall][kRadix];
+    __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
+    __shared__ uint32_t s_wave[kWaveSmall];
+    __shared__ uint32_t s_mm[2][kWaveSmall];
+    const uint32_t b0 = bkt[blockIdx.x], m = bkt[kRadix + blockIdx.x];
+    if (m == 0) return;  // uniform
+    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
+    // the bits that vary: smallest and largest key of the bucket
+    uint32_t mn = 0xffffffffu, mx = 0u;
+    for (uint32_t i = threadIdx.x; i < m; i += kRadix) {
+        const uint32_t k = kin[b0 + i];
+        mn = min(mn, k);
+        mx = max(mx, k);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) {
+        s_mm[0][wid] = mn;
+        s_mm[1][wid] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kWaveSmall; ++w) {
+        mn = min(mn, s_mm[0][w]);
+        mx = max(mx, s_mm[1][w]);
+    }
+    const uint32_t diff = mn ^ mx;
+    const int passes = diff ? (32 - __builtin_clz(diff) + 7) / 8 : 0;
+    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems], ps[kItems];
+    if (m <= kTile) {  // uniform: registers and LDS
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t pos = base + k * 64;
+            kk[k] = pos < m ? kin[b0 + pos] : 0u;
+            vv[k] = pos < m ? vin[b0 + pos] : 0u;
+        }
+        for (int p = 0; p < passes; ++p) {
+            rank_tile(kk, m, 8 * p, ps, s_cnt, s_start, s_wave, s_tdig);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if (base + k * 64 < m) {
+                    s_k[ps[k]] = kk[k];
+                    s_v[ps[k]] = vv[k];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const uint32_t pos = base + k * 64;
+                kk[k] = pos < m ? s_k[pos] : 0u;
+                vv[k] = pos < m ? s_v[pos] : 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t pos = base + k * 64;
+            if (pos < m) {
+                kout[b0 + pos] = kk[k];
+                vout[b0 + pos] = vv[k];
+            }
+        }
+        return;
+    }
+    // long bucket: LSD passes through global memory, 4096-key tiles in order
+    uint32_t *sk = kin, *sv = vin, *dk = kout, *dv = vout;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        s_run[d] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += kRadix) atomicAdd(&s_run[(sk[b0 + i] >> shift) & 0xffu], 1u);
+        __syncthreads();
+        {
+            const uint32_t c = s_run[d];
+            const uint32_t ex = block_excl_scan<kWaveSmall>(c, s_wave);
+            s_run[d] = ex;  // (each thread its own digit)
+        }
+        for (uint32_t t0 = 0; t0 < m; t0 += kTile) {
+            const uint32_t tn = min(kTile, m - t0);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const uint32_t pos = base + k * 64;
+                kk[k] = pos < tn ? sk[b0 + t0 + pos] : 0u;
+                vv[k] = pos < tn ? sv[b0 + t0 + pos] : 0u;
+            }
+            rank_tile(kk, tn, shift, ps, s_cnt, s_start, s_wave, s_tdig);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if (base + k * 64 < tn) {
+                    const uint32_t dg = (kk[k] >> shift) & 0xffu;
+                    const uint32_t o = b0 + s_run[dg] + (ps[k] - s_start[dg]);
+                    dk[o] = kk[k];
+                    dv[o] = vv[k];
+                }
+            __syncthreads();
+            s_run[d] += s_tdig[d];
+        }
+        // the pass's stores before the next pass's loads by the other waves (agent-scope
+        // release / acquire: the acquire invalidates this CU's vector L1)
+        __threadfence();
+        __syncthreads();
+        __threadfence();
+        uint32_t *t = sk;
+        sk = dk;
+        dk = t;
+        t = sv;
+        sv = dv;
+        dv = t;
+    }
+    if (sk != kout)  // uniform: an even number of passes left the bucket in (kin, vin)
+        for (uint32_t i = threadIdx.x; i < m; i += kRadix) {
+            kout[b0 + i] = kin[b0 + i];
+            vout[b0 + i] = vin[b0 + i];
+        }
 }
 
 // The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
@@ -849,6 +1048,10 @@ int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, boo
         }
         sc.hist_cap = cap;
     }
+    if (!sc.bkt && hipMalloc(&sc.bkt, 2 * kRadix * 4) != hipSuccess) {  // the bucket form's (base, count) table
+        err = "radix sort: out of device memory";
+        return GS_ERR_NOMEM;
+    }
     if (!sc.row_total) {  // row totals [256] + tile counts [16][256] + above-1e6 counts [16] (zero between sorts)
         const size_t bytes = ((size_t)(1 + kTileCopies) * kRadix + kTileCopies) * 4;
         if (hipMalloc(&sc.row_total, bytes) != hipSuccess || hipMemsetAsync(sc.row_total, 0, bytes, s) != hipSuccess) {
@@ -864,17 +1067,19 @@ void sort_free(SortScratch &sc) {
     if (sc.vals_alt) (void)hipFree(sc.vals_alt);
     if (sc.hist) (void)hipFree(sc.hist);
     if (sc.row_total) (void)hipFree(sc.row_total);
+    if (sc.bkt) (void)hipFree(sc.bkt);
     sc = SortScratch{};
 }
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out,
-               const PrefixDev *pre, int64_t dup_base, bool small) {
+               const PrefixDev *pre, int64_t dup_base, bool small, bool bucket) {
     if (dup_base >= 0 && !dev_count) {
         err = "radix sort: the split layout needs a device count";
         return GS_ERR_INVALID;
     }
     small = small && !pre && n >= 1;
+    bucket = bucket && small;
     if (pre && (!bins || !dev_count)) {
         err = "radix sort: a prefix sort needs bins and a device count";
         return GS_ERR_INVALID;
@@ -905,18 +1110,26 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         for (int pass = 0; pass < 4; ++pass) {
             const uint32_t sp = pass == 0 ? split : kNoSplit;
             hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
+            // the bucket form: pass 0 scatters by bucket (tile), then one k_bucket_sort finishes
+            // every bucket (3 launches in all)
+            const bool bk = bucket && pass == 0;
             if (pass == 0 && bins)
-                hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, true>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0,
-                                      nullptr, 0, kin, (uint32_t)n, dev_count, 0, sc.hist, nb, tile_counts, PrefixDev{},
-                                      sp, nullptr);
+                hipExtLaunchKernelGGL((bk ? k_upsweep<kWaveSmall, true, false, true> : k_upsweep<kWaveSmall, true>),
+                                      dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
+                                      dev_count, 0, sc.hist, nb, tile_counts, PrefixDev{}, sp, nullptr);
             else
-                hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0,
-                                      nullptr, 0, kin, (uint32_t)n, dev_count, 8 * pass, sc.hist, nb, nullptr,
-                                      PrefixDev{}, sp, nullptr);
+                hipExtLaunchKernelGGL((bk ? k_upsweep<kWaveSmall, false, false, true> : k_upsweep<kWaveSmall, false>),
+                                      dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
+                                      dev_count, 8 * pass, sc.hist, nb, nullptr, PrefixDev{}, sp, nullptr);
             const dim3 grid(nb + ((pass == 0 && bins) ? 1 : 0));
-            hipExtLaunchKernelGGL(k_sweep_small, grid, dim3(kWaveSmall * 64), 0, s, nullptr, e1, 0, kin, vin, kout, vout,
-                                  (uint32_t)n, dev_count, 8 * pass, sc.hist, nb, sp, tile_counts,
-                                  pass == 0 ? bins : nullptr);
+            hipExtLaunchKernelGGL((bk ? k_sweep_small<true> : k_sweep_small<false>), grid, dim3(kWaveSmall * 64), 0, s,
+                                  nullptr, bk ? nullptr : e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, 8 * pass,
+                                  sc.hist, nb, sp, tile_counts, pass == 0 ? bins : nullptr, sc.bkt);
+            if (bk) {  // (alt -> keys: the result is where the 4-pass form leaves it)
+                hipExtLaunchKernelGGL(k_bucket_sort, dim3(kRadix), dim3(kWaveSmall * 64), 0, s, nullptr, stop, 0, kout, vout, kin, vin,
+                                      sc.bkt);
+                break;
+            }
             std::swap(kin, kout);
             std::swap(vin, vout);
         }

@@ -66,6 +66,13 @@ class Context:
         sort in 8 launches (-1 leaves a limit)"""
         check(lib().gs_ctx_set_small_limits(self.handle, int(draw_entries), int(sort_entries)), self.handle)
 
+    def set_bucket_sort(self, on: int = -1) -> int:
+        """gs_ctx_set_bucket_sort: the small sort by tile then per tile (1, default) or in four
+        8-bit passes (0); -1 leaves it.  Returns the form set."""
+        r = lib().gs_ctx_set_bucket_sort(self.handle, int(on))
+        check(min(r, 0), self.handle)
+        return r
+
     def set_draw_sub(self, sub: int = -1) -> int:
         """the blend's sub-block form (gs_ctx_set_draw_sub): 0 by entry count (default), 8 (one
         pixel per lane, small frames) or 16 (2x2 quads per lane, large frames); -1 leaves it.

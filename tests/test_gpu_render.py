@@ -136,6 +136,32 @@ def test_queued_preprocess_on_mostly_culled_frames(oracle, W, H, turn, flags):
         assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{frame}/image")
 
 
+@pytest.mark.parametrize("bucket", [1, 0])
+@pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
+def test_small_sort_forms_match_oracle(oracle, bucket, flags):
+    """frames below the small-sort limit sort by tile and then each tile's list (k_bucket_sort;
+    a list over 4096 keys takes its global-memory passes) or in four 8-bit passes: keys, values,
+    bins and image bit-exact against the oracle, for an ordinary scene and one whose splats all
+    fall into a few tiles (30k-entry lists)"""
+    from openglgaussiansplattingrenderer_amd.scenes import c2_scene
+    ctx = g.Context(0)
+    assert ctx.set_bucket_sort(bucket) == bucket
+    means, rot, sc, op, col = c2_scene(30_000, seed=3)
+    c = means.mean(0)
+    for mm, ss in ((means, sc), (c + (means - c) * 0.03, sc * 0.05)):
+        sp = g.Splats.from_raw(mm.astype(np.float32), col, np.log(op / (1 - op)), np.log(ss.astype(np.float32)), rot,
+                               512, 512, ctx=ctx)
+        u = g.main_camera(512, 512).uniforms()
+        o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=flags)
+        for _ in range(2):  # the first frame of a context, then one whose predecessor's count is known
+            r = gpu_frame(sp, u, flags)
+            assert [r["V"], r["D"], r["E"]] == [o["V"], o["D"], o["E"]]
+            for k in ("keys", "vals", "bins"):
+                assert_bits(r[k], o[k], f"bucket {bucket}/{k}")
+            assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"bucket {bucket}/image")
+    ctx.set_bucket_sort(1)
+
+
 @pytest.mark.parametrize("flags", [0, g.GS_FLAG_CLEAN])
 def test_non_finite_colours_match_oracle(ctx, oracle, flags, sub):
     """splats whose colour is +-inf or NaN (f_dc non-finite): the blend keeps a pixel by selects
