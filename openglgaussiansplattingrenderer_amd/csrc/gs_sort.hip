@@ -166,13 +166,13 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t key, int shift) {
     return BKT ? bucket_of(key) : (key >> shift) & 0xffu;
 }
 
-template <int W, bool TILES, bool PREFIX = false, bool BKT = false>
+template <int W, bool TILES, bool PREFIX = false, bool BKT = false, int IT = kItems>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ tile_counts, PrefixDev pre,
                                                     uint32_t dup_base, uint32_t *__restrict__ zero_cols) {
-    constexpr int kThreads = W * 64, kTile = kThreads * kItems;
+    constexpr int kThreads = W * 64, kTile = kThreads * IT;
     static_assert(kThreads >= kRadix, "one thread per digit flushes the counts");
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
@@ -198,22 +198,22 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     if (TILES && threadIdx.x == 0) s_above = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems];
+    const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)(64 * IT) + lane;
+    uint32_t kk[IT];
     if (dup_base != kNoSplit) {  // uniform: the split emission layout
         const uint32_t v0 = cnt[0], gap = dup_base - v0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t idx = base + k * 64;
             kk[k] = (idx < n) ? keys[split_at(idx, v0, gap)] : 0u;
         }
     } else if (tile * (uint32_t)kTile + kTile <= n) {  // uniform: full tile, immediate offsets
         const uint32_t *p = keys + base;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) kk[k] = p[k * 64];
+        for (int k = 0; k < IT; ++k) kk[k] = p[k * 64];
     } else {
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t idx = base + k * 64;
             kk[k] = (idx < n) ? keys[idx] : 0u;
         }
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     const uint32_t rep = (uint32_t)lane & (kRep - 1);
     uint32_t above = 0, low = 0;
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const uint32_t idx = base + k * 64;
         if (idx < n) {
             bool keep = true;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
 // (returns the tile's count and the exclusive prefix; *s_above gets the keys above 1e6)
 __device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w,
                            uint32_t *s_above) {
-    __shared__ uint32_t s_c[kRadix];
+    __shared__ __attribute__((aligned(16))) uint32_t s_c[kRadix];
     const int t = threadIdx.x;
     uint32_t v = 0;
 #pragma unroll
@@ -304,12 +304,26 @@ __device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__
     uint32_t tot;
     const uint32_t ex = block_excl_scan_tot<4>(v, s_w, &tot);  // (its barriers also publish s_c)
     bins[t] = ex + v;
-    // rank = #tiles ahead of t: longer, or as long with a smaller index
+    // rank = #tiles ahead of t: longer, or as long with a smaller index.  With every count below
+    // 2^24 (tot < 2^24; uniform) the order is that of one word, count << 8 | (255 - tile):
+    // one compare per tile, four tiles per LDS read
     uint32_t r = 0;
+    if (tot < (1u << 24)) {
+        s_c[t] = (v << 8) | (uint32_t)(255 - t);  // (each thread rewrites its own word)
+        __syncthreads();
+        const uint32_t key = (v << 8) | (uint32_t)(255 - t);
+        const uint4 *q = reinterpret_cast<const uint4 *>(s_c);
+#pragma unroll 16
+        for (int u = 0; u < kRadix / 4; ++u) {
+            const uint4 c = q[u];
+            r += (c.x > key ? 1u : 0u) + (c.y > key ? 1u : 0u) + (c.z > key ? 1u : 0u) + (c.w > key ? 1u : 0u);
+        }
+    } else {
 #pragma unroll 32
-    for (int u = 0; u < kRadix; ++u) {
-        const uint32_t c = s_c[u];
-        r += (c > v || (c == v && u < t)) ? 1u : 0u;
+        for (int u = 0; u < kRadix; ++u) {
+            const uint32_t c = s_c[u];
+            r += (c > v || (c == v && u < t)) ? 1u : 0u;
+        }
     }
     bins[kRadix + r] = (uint32_t)t;
     return make_uint2(v, ex);
@@ -665,7 +679,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
 // was small (kSmallSortEntries).  Tiles of 4096 keys (4 waves).
 // BKT: the bucket sort's first pass (digit = bucket_of(key)); the workgroup of tile 0 also writes
 // each bucket's (base, count) to bkt[d], bkt[256 + d] for k_bucket_sort.
-template <bool BKT>
+template <bool BKT, int IT = kItems>
 __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t *__restrict__ kin,
                                                                const uint32_t *__restrict__ vin,
                                                                uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
@@ -673,7 +687,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
                                                                int shift, const uint32_t *__restrict__ hist, uint32_t nb,
                                                                uint32_t dup_base, uint32_t *__restrict__ tile_counts,
                                                                uint32_t *__restrict__ bins, uint32_t *__restrict__ bkt) {
-    constexpr int kThreads = kWaveSmall * 64, kTile = kThreads * kItems, kWaves = kWaveSmall;
+    constexpr int kThreads = kWaveSmall * 64, kTile = kThreads * IT, kWaves = kWaveSmall;
     static_assert(kThreads == kRadix, "one thread per digit");
     __shared__ uint32_t s_w[4];
     if (bins && blockIdx.x == gridDim.x - 1) {  // uniform: the bins workgroup (first pass)
@@ -695,12 +709,12 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t tile0 = tile * (uint32_t)kTile;
-    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems], vv[kItems];
+    const uint32_t base = tile0 + wid * (uint32_t)(64 * IT) + lane;
+    uint32_t kk[IT], vv[IT];
     {
         const uint32_t v0 = dup_base != kNoSplit ? cnt[0] : 0xffffffffu, gap = dup_base - v0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t idx = base + k * 64;
             const uint32_t a = split_at(idx, v0, gap);
             kk[k] = (idx < n) ? kin[a] : 0u;
@@ -731,9 +745,9 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
             }
         }
     }
-    uint32_t rank[kItems], lead[kItems], old[kItems];
+    uint32_t rank[IT], lead[IT], old[IT];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const bool valid = base + k * 64 < n;
         const uint32_t dg = digit_of<BKT>(kk[k], shift);
         const uint64_t m = match_digit(dg, __ballot(valid));
@@ -742,12 +756,12 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
         old[k] = valid ? (uint32_t)__popcll(m) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const bool valid = base + k * 64 < n;
         if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][digit_of<BKT>(kk[k], shift)], old[k]);
     }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    for (int k = 0; k < IT; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
     __syncthreads();
     {
         uint32_t tot = 0;
@@ -768,7 +782,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         if (base + k * 64 < n) {
             const uint32_t dg = digit_of<BKT>(kk[k], shift);
             const uint32_t pos = s_start[dg] + s_cnt[wid][dg] + rank[k];
@@ -786,11 +800,12 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     }
 }
 
-// Stable ranks of one tile of up to 4096 keys held as k_sweep_small holds them (4 waves: wave w,
-// item k, lane l is position w*1024 + k*64 + l; valid below tn): ps[k] = the item's place in the
+// Stable ranks of one tile of up to 256 * IT keys held as k_sweep_small holds them (4 waves:
+// wave w, item k, lane l is position w*64*IT + k*64 + l; valid below tn): ps[k] = the item's place in the
 // tile's order by digit (key >> shift) & 0xff; s_tdig[d] = the tile's count of digit d, and
 // s_start[d] its first place.  Starts and ends with a barrier.
-__device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t tn, int shift, uint32_t (&ps)[kItems],
+template <int IT>
+__device__ __forceinline__ void rank_tile(const uint32_t (&kk)[IT], uint32_t tn, int shift, uint32_t (&ps)[IT],
                                           uint32_t (*s_cnt)[kRadix], uint32_t *s_start, uint32_t *s_wave,
                                           uint32_t *s_tdig) {
     const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
@@ -798,10 +813,10 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t
 #pragma unroll
     for (int w = 0; w < kWaveSmall; ++w) s_cnt[w][d] = 0;
     __syncthreads();
-    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
-    uint32_t rank[kItems], lead[kItems], old[kItems];
+    const uint32_t base = wid * (uint32_t)(64 * IT) + lane;
+    uint32_t rank[IT], lead[IT], old[IT];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const bool valid = base + k * 64 < tn;
         const uint64_t m = match_digit((kk[k] >> shift) & 0xffu, __ballot(valid));
         rank[k] = count_below(m);
@@ -809,12 +824,12 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t
         old[k] = valid ? (uint32_t)__popcll(m) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const bool valid = base + k * 64 < tn;
         if (valid && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);
     }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    for (int k = 0; k < IT; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
     __syncthreads();
     uint32_t tot = 0;
 #pragma unroll
@@ -827,7 +842,7 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t
     s_start[d] = block_excl_scan<kWaveSmall>(tot, s_wave);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const uint32_t dg = (kk[k] >> shift) & 0xffu;
         ps[k] = s_start[dg] + s_cnt[wid][dg] + rank[k];
     }
@@ -841,25 +856,16 @@ __device__ __forceinline__ void rank_tile(const uint32_t (&kk)[kItems], uint32_t
 // a tile >= 128's keys 2) order it completely.  Buckets of <= 4096 keys sort in registers and
 // LDS; longer ones (rare: a tile list that long in a frame this small) take the same passes
 // through global memory in 4096-key tiles, ping-ponging between the two arrays' bucket ranges.
-__global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__restrict__ kin, uint32_t *__restrict__ vin,
-                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                               const uint32_t *__restrict__ bkt) {
-    static_assert(kWaveSmall * 64 == kRadix, "one thread per digit");
-    constexpr uint32_t kTile = kTileSmall;
-    __shared__ uint32_t s_k[kTile], s_v[kTile];
-    __shared__ uint32_t s_cnt[kWaveSmall][kRadix];
-    __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
-    __shared__ uint32_t s_wave[kWaveSmall];
-    __shared__ uint32_t s_mm[2][kWaveSmall];
-    const uint32_t b0 = bkt[blockIdx.x], m = bkt[kRadix + blockIdx.x];
-    if (m == 0) return;  // uniform
-    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
-    // the bits that vary: smallest and largest key of the bucket
+// the bits of a bucket that vary (the smallest and largest key of it, over the workgroup; kk: each
+// thread's keys, invalid ones neutral) -> the LSD passes needed
+template <int IT>
+__device__ __forceinline__ int bucket_passes(const uint32_t (&kmin)[IT], const uint32_t (&kmax)[IT], uint32_t (*s_mm)[kWaveSmall]) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
     uint32_t mn = 0xffffffffu, mx = 0u;
-    for (uint32_t i = threadIdx.x; i < m; i += kRadix) {
-        const uint32_t k = kin[b0 + i];
-        mn = min(mn, k);
-        mx = max(mx, k);
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        mn = min(mn, kmin[k]);
+        mx = max(mx, kmax[k]);
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -877,42 +883,95 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
         mx = max(mx, s_mm[1][w]);
     }
     const uint32_t diff = mn ^ mx;
-    const int passes = diff ? (32 - __builtin_clz(diff) + 7) / 8 : 0;
-    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems], vv[kItems], ps[kItems];
-    if (m <= kTile) {  // uniform: registers and LDS
+    return diff ? (32 - __builtin_clz(diff) + 7) / 8 : 0;
+}
+
+// a bucket of m <= 256 * IT keys: registers and LDS (s_k, s_v hold 256 * IT)
+template <int IT>
+__device__ __forceinline__ void bucket_fast(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t b0,
+                                            uint32_t m, uint32_t *s_k, uint32_t *s_v, uint32_t (*s_cnt)[kRadix],
+                                            uint32_t *s_start, uint32_t *s_wave, uint32_t *s_tdig,
+                                            uint32_t (*s_mm)[kWaveSmall]) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t base = wid * (uint32_t)(64 * IT) + lane;
+    uint32_t kk[IT], vv[IT], ps[IT], kmn[IT], kmx[IT];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const uint32_t pos = base + k * 64;
-            kk[k] = pos < m ? kin[b0 + pos] : 0u;
-            vv[k] = pos < m ? vin[b0 + pos] : 0u;
-        }
-        for (int p = 0; p < passes; ++p) {
-            rank_tile(kk, m, 8 * p, ps, s_cnt, s_start, s_wave, s_tdig);
+    for (int k = 0; k < IT; ++k) {
+        const uint32_t pos = base + k * 64;
+        kk[k] = pos < m ? kin[b0 + pos] : 0u;
+        vv[k] = pos < m ? vin[b0 + pos] : 0u;
+    }
 #pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if (base + k * 64 < m) {
-                    s_k[ps[k]] = kk[k];
-                    s_v[ps[k]] = vv[k];
-                }
-            __syncthreads();
+    for (int k = 0; k < IT; ++k) {
+        const bool ok = base + k * 64 < m;
+        kmn[k] = ok ? kk[k] : 0xffffffffu;
+        kmx[k] = ok ? kk[k] : 0u;
+    }
+    const int passes = bucket_passes<IT>(kmn, kmx, s_mm);
+    for (int p = 0; p < passes; ++p) {
+        rank_tile<IT>(kk, m, 8 * p, ps, s_cnt, s_start, s_wave, s_tdig);
 #pragma unroll
-            for (int k = 0; k < kItems; ++k) {
-                const uint32_t pos = base + k * 64;
-                kk[k] = pos < m ? s_k[pos] : 0u;
-                vv[k] = pos < m ? s_v[pos] : 0u;
+        for (int k = 0; k < IT; ++k)
+            if (base + k * 64 < m) {
+                s_k[ps[k]] = kk[k];
+                s_v[ps[k]] = vv[k];
             }
-        }
+        __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t pos = base + k * 64;
-            if (pos < m) {
-                kout[b0 + pos] = kk[k];
-                vout[b0 + pos] = vv[k];
-            }
+            kk[k] = pos < m ? s_k[pos] : 0u;
+            vv[k] = pos < m ? s_v[pos] : 0u;
         }
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const uint32_t pos = base + k * 64;
+        if (pos < m) {
+            kout[b0 + pos] = kk[k];
+            vout[b0 + pos] = vv[k];
+        }
+    }
+}
+
+// (bins != null: one more workgroup, the last, scans the frame's tile counts into the bins --
+// here rather than beside the scatter, whose duration it set at C2)
+__global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__restrict__ kin, uint32_t *__restrict__ vin,
+                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                               const uint32_t *__restrict__ bkt,
+                                                               uint32_t *__restrict__ tile_counts,
+                                                               uint32_t *__restrict__ bins) {
+    static_assert(kWaveSmall * 64 == kRadix, "one thread per digit");
+    constexpr uint32_t kTile = kTileSmall;
+    if (bins && blockIdx.x == kRadix) {  // uniform: the bins workgroup
+        __shared__ uint32_t s_w[4], s_above;
+        bins_scan(tile_counts, bins, s_w, &s_above);
         return;
     }
+    __shared__ uint32_t s_k[kTile], s_v[kTile];
+    __shared__ uint32_t s_cnt[kWaveSmall][kRadix];
+    __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
+    __shared__ uint32_t s_wave[kWaveSmall];
+    __shared__ uint32_t s_mm[2][kWaveSmall];
+    const uint32_t b0 = bkt[blockIdx.x], m = bkt[kRadix + blockIdx.x];
+    if (m == 0) return;  // uniform
+    // (uniform) short buckets with 4 keys per lane, up to 4096 with 16
+    if (m <= kTile / 4) return bucket_fast<kItems / 4>(kin, vin, kout, vout, b0, m, s_k, s_v, s_cnt, s_start, s_wave, s_tdig, s_mm);
+    if (m <= kTile) return bucket_fast<kItems>(kin, vin, kout, vout, b0, m, s_k, s_v, s_cnt, s_start, s_wave, s_tdig, s_mm);
+    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
+    int passes;
+    {
+        uint32_t mn[1] = {0xffffffffu}, mx[1] = {0u};
+        for (uint32_t i = threadIdx.x; i < m; i += kRadix) {
+            const uint32_t k = kin[b0 + i];
+            mn[0] = min(mn[0], k);
+            mx[0] = max(mx[0], k);
+        }
+        passes = bucket_passes<1>(mn, mx, s_mm);
+    }
+    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems], ps[kItems];
     // long bucket: LSD passes through global memory, 4096-key tiles in order
     uint32_t *sk = kin, *sv = vin, *dk = kout, *dv = vout;
     for (int p = 0; p < passes; ++p) {
@@ -934,7 +993,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
                 kk[k] = pos < tn ? sk[b0 + t0 + pos] : 0u;
                 vv[k] = pos < tn ? sv[b0 + t0 + pos] : 0u;
             }
-            rank_tile(kk, tn, shift, ps, s_cnt, s_start, s_wave, s_tdig);
+            rank_tile<kItems>(kk, tn, shift, ps, s_cnt, s_start, s_wave, s_tdig);
 #pragma unroll
             for (int k = 0; k < kItems; ++k)
                 if (base + k * 64 < tn) {
@@ -1023,7 +1082,9 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small) {
     // the most tiles of any pass (the small form keeps all four passes' histograms)
-    const size_t nb = (size_t)((n + kTileSmall - 1) / kTileSmall) + 3;  // (+3: the small form's 16-byte rows)
+    // (small: the bucket pass's 1024-key tiles)
+    const size_t tsz = small ? kTileSmall / 4 : kTileSmall;
+    const size_t nb = (size_t)((n + tsz - 1) / tsz) + 3;  // (+3: the small form's 16-byte rows)
     const bool grow_alt = (size_t)n > sc.alt_cap, grow_hist = nb * kRadix > sc.hist_cap;
     if ((grow_alt && sc.keys_alt) || (grow_hist && sc.hist)) (void)hipStreamSynchronize(s);  // in-flight users
     if (grow_alt) {
@@ -1104,7 +1165,13 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
     }
     if (small) {  // the small form (k_sweep_small): 8 launches, keys and values out
-        const uint32_t nb = (uint32_t)((n + kTileSmall - 1) / kTileSmall + 3) & ~3u;  // row stride: 16-byte rows
+        // (the bucket pass of up to 192k keys -- n is the capacity for a frame counted on the
+        // device -- in 1024-key tiles: 4x the workgroups, each a quarter of the serial work; above
+        // that the per-workgroup reads of the histogram rows, O(tiles), outweigh it: C5 view 2,
+        // 383k keys, sort 0.043 -> 0.056 ms)
+        const bool t1k = bucket && n <= (192 << 10);
+        const uint32_t tsz = t1k ? kTileSmall / 4 : kTileSmall;
+        const uint32_t nb = (uint32_t)((n + tsz - 1) / tsz + 3) & ~3u;  // row stride: 16-byte rows
         const uint32_t split = dup_base >= 0 ? (uint32_t)dup_base : kNoSplit;
         uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
         for (int pass = 0; pass < 4; ++pass) {
@@ -1113,21 +1180,22 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
             // the bucket form: pass 0 scatters by bucket (tile), then one k_bucket_sort finishes
             // every bucket (3 launches in all)
             const bool bk = bucket && pass == 0;
-            if (pass == 0 && bins)
-                hipExtLaunchKernelGGL((bk ? k_upsweep<kWaveSmall, true, false, true> : k_upsweep<kWaveSmall, true>),
-                                      dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
-                                      dev_count, 0, sc.hist, nb, tile_counts, PrefixDev{}, sp, nullptr);
-            else
-                hipExtLaunchKernelGGL((bk ? k_upsweep<kWaveSmall, false, false, true> : k_upsweep<kWaveSmall, false>),
-                                      dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
-                                      dev_count, 8 * pass, sc.hist, nb, nullptr, PrefixDev{}, sp, nullptr);
-            const dim3 grid(nb + ((pass == 0 && bins) ? 1 : 0));
-            hipExtLaunchKernelGGL((bk ? k_sweep_small<true> : k_sweep_small<false>), grid, dim3(kWaveSmall * 64), 0, s,
-                                  nullptr, bk ? nullptr : e1, 0, kin, vin, kout, vout, (uint32_t)n, dev_count, 8 * pass,
-                                  sc.hist, nb, sp, tile_counts, pass == 0 ? bins : nullptr, sc.bkt);
+            auto up = pass == 0 && bins
+                          ? (bk ? (t1k ? k_upsweep<kWaveSmall, true, false, true, kItems / 4> : k_upsweep<kWaveSmall, true, false, true>)
+                                : k_upsweep<kWaveSmall, true>)
+                          : (bk ? (t1k ? k_upsweep<kWaveSmall, false, false, true, kItems / 4> : k_upsweep<kWaveSmall, false, false, true>)
+                                : k_upsweep<kWaveSmall, false>);
+            hipExtLaunchKernelGGL(up, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
+                                  dev_count, 8 * pass, sc.hist, nb, pass == 0 && bins ? tile_counts : nullptr, PrefixDev{}, sp,
+                                  nullptr);
+            const dim3 grid(nb + ((pass == 0 && bins && !bk) ? 1 : 0));
+            auto sw = bk ? (t1k ? k_sweep_small<true, kItems / 4> : k_sweep_small<true>) : k_sweep_small<false>;
+            hipExtLaunchKernelGGL(sw, grid, dim3(kWaveSmall * 64), 0, s, nullptr, bk ? nullptr : e1, 0, kin, vin, kout, vout,
+                                  (uint32_t)n, dev_count, 8 * pass, sc.hist, nb, sp, tile_counts,
+                                  pass == 0 && !bk ? bins : nullptr, sc.bkt);
             if (bk) {  // (alt -> keys: the result is where the 4-pass form leaves it)
-                hipExtLaunchKernelGGL(k_bucket_sort, dim3(kRadix), dim3(kWaveSmall * 64), 0, s, nullptr, stop, 0, kout, vout, kin, vin,
-                                      sc.bkt);
+                hipExtLaunchKernelGGL(k_bucket_sort, dim3(kRadix + (bins ? 1 : 0)), dim3(kWaveSmall * 64), 0, s, nullptr, stop, 0,
+                                      kout, vout, kin, vin, sc.bkt, tile_counts, bins);
                 break;
             }
             std::swap(kin, kout);
