@@ -186,8 +186,8 @@ SORT_BIG_N = 64 << 20  # 64M pairs: 512 MB of (key, value), 1.28 GB with the alt
 def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
     """The same pair sort beyond the caches: 64M uniform 32-bit keys (HBM-resident), median of
     `reps` hipEvent-timed sorts; algorithmic bytes 68 B/key; counter-based bytes from
-    the committed rocprofv3 calibration (profiles/r02/calibration.txt: 88.1 B/key measured by
-    FETCH_SIZE x2 + WRITE_SIZE at this size)."""
+    the committed rocprofv3 measurement (profiles/r03/sort_64M.txt: 83.4 B/key by FETCH_SIZE x2 +
+    WRITE_SIZE at this size, with the r02 gather calibration's reading of the counters)."""
     import openglgaussiansplattingrenderer_amd as g
     n = SORT_BIG_N
     rng = np.random.default_rng(64)
@@ -206,13 +206,13 @@ def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
     k_out = kb.download(np.uint32, n)
     ok = bool(np.all(k_out[1:] >= k_out[:-1]))
     med = float(np.median(ms))
-    b_counter = 88.1  # B/key, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE (profiles/r02/calibration.txt)
+    b_counter = 83.4  # B/key, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this sort (profiles/r03/sort_64M.txt)
     return dict(n=n, keys="uniform 32-bit, seeded", ms_pairs=round(med, 4), gkeys_per_s=round(n / med / 1e6, 2),
                 hbm_frac_algorithmic=round(68.0 * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 hbm_frac_counters=round(b_counter * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 counter_bytes_per_key=b_counter, sorted_ok=ok,
-                source="hipEvents around gs_sort_pairs_u32 (12 kernels); 68 B/key algorithmic, 88.1 B/key by "
-                       "counters (profiles/r02/calibration.txt)")
+                source="hipEvents around gs_sort_pairs_u32 (12 kernels); 68 B/key algorithmic, 83.4 B/key by "
+                       "counters (profiles/r03/sort_64M.txt)")
 
 
 def cpu_baseline(sp, u, flags, budget_s: float = 20.0):

@@ -440,13 +440,15 @@ __device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restric
 // One workgroup of 256 per digit (a small workgroup finds room on a CU beside the previous
 // frame's blend; 1024-thread ones waited for a CU to drain): exclusive scan of that digit's
 // per-tile counts (the tiles holding elements; rows are nb long), row total.  Each thread owns
-// 16 consecutive counts per round, so a round (4096 tiles = 16.7M keys) costs one memory round
-// trip.  With bins != null, block kRadix computes the tile bins from tile_counts instead.
+// kPer consecutive counts per round, so a round (256 * kPer tiles) costs one memory round
+// trip: kPer 16 (4096 tiles = 16.7M keys) for frames, 64 with 16-byte loads for sorts beyond
+// that (64M keys: one round instead of four, 28 -> ? us per pass).  With bins != null, block
+// kRadix computes the tile bins from tile_counts instead.
+template <int kPer = 16>
 __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
                                                    uint32_t *__restrict__ bins, PrefixDev pre, int prefix) {
-    constexpr int kPer = 16;
     __shared__ uint32_t s_w[4];
     if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
         if (prefix == 1) {
@@ -465,16 +467,42 @@ __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, 
     for (uint32_t b = 0; b < nb; b += 256 * kPer) {
         const uint32_t i0 = b + threadIdx.x * kPer;
         uint32_t v[kPer], a = 0;
+        if (kPer > 16 && (nb_stride & 3u) == 0 && i0 + kPer <= nb) {  // whole 16-byte groups (row start aligned)
+            const uint4 *r4 = reinterpret_cast<const uint4 *>(row + i0);
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) v[k] = (i0 + k < nb) ? row[i0 + k] : 0u;
+            for (int k = 0; k < kPer / 4; ++k) {
+                const uint4 q = r4[k];
+                v[4 * k] = q.x, v[4 * k + 1] = q.y, v[4 * k + 2] = q.z, v[4 * k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) v[k] = (i0 + k < nb) ? row[i0 + k] : 0u;
+        }
 #pragma unroll
         for (int k = 0; k < kPer; ++k) a += v[k];
         uint32_t tot;
         uint32_t off = carry + block_excl_scan_tot<4>(a, s_w, &tot);
+        if (kPer > 16 && (nb_stride & 3u) == 0 && i0 + kPer <= nb) {
+            uint4 *r4 = reinterpret_cast<uint4 *>(row + i0);
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            if (i0 + k < nb) row[i0 + k] = off;
-            off += v[k];
+            for (int k = 0; k < kPer / 4; ++k) {
+                uint4 q;
+                q.x = off;
+                off += v[4 * k];
+                q.y = off;
+                off += v[4 * k + 1];
+                q.z = off;
+                off += v[4 * k + 2];
+                q.w = off;
+                off += v[4 * k + 3];
+                r4[k] = q;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                if (i0 + k < nb) row[i0 + k] = off;
+                off += v[k];
+            }
         }
         carry += tot;
     }
@@ -1159,7 +1187,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     uint32_t *tile_counts = sc.row_total + kRadix;
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
         if (start) (void)hipEventRecord(start, s);
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
+        hipLaunchKernelGGL(k_scan_rows<>, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, 0u, 0u, nullptr, 1u, sc.row_total,
                            tile_counts, bins, PrefixDev{}, 0);
         if (stop) (void)hipEventRecord(stop, s);
         return hipGetLastError() == hipSuccess ? GS_OK : GS_ERR_HIP;
@@ -1215,9 +1243,14 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
         start = nullptr;
     }
+    // passes 1-3 in the pass-0 form (8 waves, 8192-key tiles) too for sorts of 16M keys or more:
+    // 64M pairs, downsweep 272 -> 232 us and upsweep 75 -> 54 us per pass (a frame's kept keys,
+    // ~2M, ran 3 % slower that way; 12- and 16-wave tiles spill: 2.8 / 3.5 ms against 1.20)
+    // (standalone pair sorts: no bins, pairs out in every pass)
+    const bool all_big = !pre && !bins && keys_out && n >= (int64_t)1 << 24;
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
-        const bool big = pass == 0;
+        const bool big = pass == 0 || all_big;
         const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
         // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
         const uint32_t *cnt = pre && pass > 0 ? pre->nsel : dev_count;
@@ -1243,8 +1276,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         // limits; and one in the first pass makes the class tables passes 1-3 need)
         const bool with_bins = bins && (pass == 3 || (pre && pass == 0));
         const int pmode = !pre ? 0 : pass == 0 ? 1 : 2;
-        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)np,
-                           cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pmode);
+        hipLaunchKernelGGL(nb > 4096 ? k_scan_rows<64> : k_scan_rows<16>, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s,
+                           sc.hist, nb, (uint32_t)np, cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd,
+                           pmode);
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
