@@ -39,6 +39,10 @@ constexpr int kFusedMaxBlocks = 64;
 // ... and sort in 8 launches instead of 12 (k_sweep_small: each sweep sums its histogram rows
 // itself, which costs a round trip per 64 tiles of 4096 entries)
 constexpr int64_t kSmallSortEntries = 512 << 10;
+// per-tile prefix depths from the blends' reach (gs::PrefixDev::depth); 0: the configured target everywhere
+#ifndef GS_PREFIX_DEPTH
+#define GS_PREFIX_DEPTH 1
+#endif
 
 // A frame lane: a stream and the per-frame buffers of the frames it runs.  Consecutive frames
 // alternate between the ctx's lanes (two by default), so frame k+1's preprocess, emission and
@@ -158,7 +162,10 @@ struct gs_ctx {
     // seen) blend in 8x8 sub-blocks (draw_sub 0) and sort in 8 launches (k_sweep_small)
     int64_t small_draw_entries = kSmallDrawEntries;
     int64_t small_sort_entries = kSmallSortEntries;
-    bool bucket_sort = true;  // the small sort form: by tile, then per tile (3 launches); else 8 launches
+    bool bucket_sort = true;
+    // [256] per tile: the deepest window position recent blends reached (gs::PrefixDev::depth);
+    // allocated with the first prefix-sorted frame, shared by the lanes
+    uint32_t *prefix_depth = nullptr;  // the small sort form: by tile, then per tile (3 launches); else 8 launches
 };
 
 struct gs_scene {
@@ -538,6 +545,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
         if (ln.stream) (void)hipStreamDestroy(ln.stream);
     }
     if (ctx->draw_stats) (void)hipFree(ctx->draw_stats);
+    if (ctx->prefix_depth) (void)hipFree(ctx->prefix_depth);
     if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
     for (auto &set : ctx->ev)
         for (auto &e : set)
@@ -1043,6 +1051,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.n = scene->n;
     P.V = (int32_t)ctx->V;  // used when count is null (the frame's counts are on the host)
     P.prefix = prefix ? 1 : 0;
+    P.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;  // (every blend of the context refreshes the per-tile depths)
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other
@@ -1120,6 +1129,11 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
                                  : (int64_t)ctx->prefix_kept;
         pd.cap_sel = (uint32_t)(ctx->prefix_kept ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536) : cap_e);
         pd.target = (uint32_t)ctx->prefix_target;
+        if (!ctx->prefix_depth) {  // (zeroed before any frame can read it)
+            GS_HIP(ctx, hipMalloc(&ctx->prefix_depth, 256 * 4));
+            GS_HIP(ctx, hipMemset(ctx->prefix_depth, 0, 256 * 4));
+        }
+        pd.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
     }

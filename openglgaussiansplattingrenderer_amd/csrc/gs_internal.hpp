@@ -84,9 +84,14 @@ struct PrefixDev {
     const uint32_t *frame_count;  // the frame's device (V, D) (set by sort_pairs)
     uint32_t *h_slot;  // mapped pinned ring slot of the frame: [3] = kept keys (diagnostics), or null
     uint32_t target;   // entries per class to keep at least
+    // [256] per tile: the deepest window position any recent blend of the context reached
+    // (k_draw's atomicMax; decayed by 1/16 here each frame), or null.  A tile's target is then
+    // min(target, 2 * depth + kPrefixDepthSlack): lists the blends read shallowly keep less.
+    uint32_t *depth;
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };
+constexpr uint32_t kPrefixDepthSlack = 4096;
 constexpr uint32_t kKey1Bits = 0x3f800000u;    // bits(1.0f)
 constexpr uint32_t kKey256Bits = 0x43800000u;  // bits(256.0f)
 // key class: t for the keys in [t, t+1), t < 256; 256 for every other bit pattern
@@ -141,6 +146,7 @@ struct DrawParams {
     int32_t n;                  // splats of the scene
     int32_t V;                  // splats with entries (when count is null; else count[0])
     int32_t prefix;             // prefix-sorted frame: windows end at bins[kBinsLimit + t] (a miss flags fr.h_totals[2])
+    uint32_t *depth;            // [256] or null: each block atomicMax-es the window depth it reached (PrefixDev::depth)
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
 };

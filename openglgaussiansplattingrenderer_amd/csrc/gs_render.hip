@@ -1716,6 +1716,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         }
     }
     if (P.prefix && end < wend && !all_done && fr_h_totals) fr_h_totals[2] = 1u;  // (uniform) a prefix miss
+    // the depth this block's walk reached (the next frames' per-tile prefix targets)
+    if (P.depth && lane == 0) atomicMax(&P.depth[t], (uint32_t)max(0, min(base, end) - start));
     if constexpr (SMALL) {  // the lane's pixel (coordinates again from the lane id, see below)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + (l2 & 7), qy = y0 + (l2 >> 3);

@@ -1063,6 +1063,7 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t c = blockIdx.x, j = threadIdx.x;
     static_assert(kB == 8, "prefix_slot puts bucket 8j + k at word k * (kPrefixBuckets / 8) + j");
     uint32_t v[kB] = {};
+    const uint32_t dep = pre.depth ? pre.depth[c] : 0u;
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;
@@ -1078,10 +1079,14 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     uint32_t tot;
     const uint32_t ex = block_excl_scan_tot<4>(a, s_w, &tot);
     const uint32_t above = tot - ex - a;  // samples in the buckets of the higher threads
-    const uint32_t tgt = (pre.target + kPrefixSample - 1) / kPrefixSample;
+    // the class's target: the configured one, or less where recent blends read the list
+    // shallowly (the depth word was read before the scan's barriers; its decay written after)
+    const uint32_t target = dep ? min(pre.target, 2u * dep + kPrefixDepthSlack) : pre.target;
+    if (pre.depth && j == 0) pre.depth[c] = dep - (dep >> 4);
+    const uint32_t tgt = (target + kPrefixSample - 1) / kPrefixSample;
     const uint32_t hi = class_hi(c);
     if (c == 0 && j == 0) pre.theta[256] = 0xffffffffu;  // class 256 is kept whole
-    if (pre.target == 0 || tot < tgt) {
+    if (target == 0 || tot < tgt) {
         if (j == 0) pre.theta[c] = hi - 1u;  // the whole class
         return;
     }

@@ -270,3 +270,38 @@ def test_prefix_on_a_fused_frame():
         render_sync(sp, pose(W, H, k), ref)
         assert np.array_equal(outs[k].download(np.uint8, W * H * 4), ref.download(np.uint8, W * H * 4)), f"frame {k}"
     ctx.close()
+
+
+def test_prefix_depth_follows_the_blend():
+    """Per-tile depths: each blend records how deep its sub-blocks walked every tile list, and the
+    next frames keep min(target, 2 x that + 4096) entries of each list.  At C3 static frames keep
+    far fewer entries than the first (which knew no depths); a camera sweep (lists deepening and
+    shallowing) still gives every image bit for bit as the host-synchronous full sort."""
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    render_sync(sp, pose(W, H, 0), ref)
+    assert ctx.set_sort_prefix() == 32768
+    ctx.prefix_stats(reset=True)
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    kept = []
+    for _ in range(6):
+        render_spec(sp, pose(W, H, 0), out)
+        kept.append(ctx.prefix_stats()["kept"])
+    assert kept[-1] < kept[0] * 3 // 4, kept
+    img0 = out.download(np.uint8, W * H * 4)
+    render_sync(sp, pose(W, H, 0), ref)
+    assert np.array_equal(img0, ref.download(np.uint8, W * H * 4))
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    ks = [0, 2, 5, 9, 5, 1, 0, 7]
+    got = []
+    for i, k in enumerate(ks):
+        render_spec(sp, pose(W, H, k), outs[i % 3])
+        if i % 3 == 2 or i == len(ks) - 1:
+            ctx.sync()
+            got += [outs[j].download(np.uint8, W * H * 4) for j in range(i % 3 + 1)]
+    for i, k in enumerate(ks):
+        render_sync(sp, pose(W, H, k), ref)
+        assert np.array_equal(got[i], ref.download(np.uint8, W * H * 4)), f"frame {i} (pose {k})"
+    ctx.close()
