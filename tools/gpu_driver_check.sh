@@ -11,4 +11,4 @@ tail -1 $O/dc_smoke.log
 timeout -k 10 300 python bench.py > $O/dc_bench.json 2> $O/dc_bench.err || { echo BENCH_FAIL; tail -5 $O/dc_bench.err; exit 1; }
 python3 -c "
 import json; d = json.load(open('$O/dc_bench.json'))
-print('bench', d['value'], d['unit'], 'draw', d['roofline']['one_frame']['avg_launch_ms'], 'cpu', d['cpu_baseline']['value'])"
+print('bench', d['value'], d['unit'], 'draw', d['roofline']['avg_launch_ms'], 'frac', d['roofline']['frac'], 'cpu', d['cpu_baseline']['value'])"
