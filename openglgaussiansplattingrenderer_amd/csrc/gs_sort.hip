@@ -444,13 +444,15 @@ __device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restric
 // trip: kPer 16 (4096 tiles = 16.7M keys) for frames, 64 with 16-byte loads for sorts beyond
 // that (64M keys: one round instead of four, 28 -> ? us per pass).  With bins != null, block
 // kRadix computes the tile bins from tile_counts instead.
-template <int kPer = 16>
+// BINS false (a pass without the bins workgroup): none of its LDS and a few VGPRs -- 16 bytes
+// of LDS and kPer 4 fit beside seven blend waves per SIMD, so another frame's blend leaves room
+template <int kPer = 16, bool BINS = true>
 __global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
                                                    uint32_t *__restrict__ bins, PrefixDev pre, int prefix) {
     __shared__ uint32_t s_w[4];
-    if (blockIdx.x == kRadix) {  // uniform: the bins workgroup
+    if (BINS && blockIdx.x == kRadix) {  // uniform: the bins workgroup
         if (prefix == 1) {
             prefix_counts(tile_counts, pre, cnt, n_max, s_w);
         } else if (prefix == 2) {
@@ -1281,9 +1283,15 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         // limits; and one in the first pass makes the class tables passes 1-3 need)
         const bool with_bins = bins && (pass == 3 || (pre && pass == 0));
         const int pmode = !pre ? 0 : pass == 0 ? 1 : 2;
-        hipLaunchKernelGGL(nb > 4096 ? k_scan_rows<64> : k_scan_rows<16>, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s,
-                           sc.hist, nb, (uint32_t)np, cnt, tile, sc.row_total, tile_counts, with_bins ? bins : nullptr, pd,
-                           pmode);
+#ifndef GS_SCAN_LIGHT
+#define GS_SCAN_LIGHT 1
+#endif
+        auto scan = with_bins ? (nb > 4096 ? k_scan_rows<64> : k_scan_rows<16>)
+                    : nb > 4096  ? k_scan_rows<64, false>
+                    : (GS_SCAN_LIGHT && nb <= 1024) ? k_scan_rows<4, false>
+                                                    : k_scan_rows<16, false>;
+        hipLaunchKernelGGL(scan, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)np, cnt, tile,
+                           sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pmode);
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
