@@ -149,29 +149,51 @@ __device__ __forceinline__ float sh_channel_k(const float *k, float x, float y, 
     r = r + 0.5f;
     return fmaxf(r, 0.0f) * 255.0f;
 }
+// The scene's SH layout (gs_scene_set_sh): groups of 64 splats; within a group, quad q (the
+// coefficients 4q..4q+3 of the 48, channel-major: 16c + j) of the 64 splats is 1 KB contiguous,
+// so a wave reading quad q of its 64 splats reads 1 KB in one coalesced 16-byte load per lane,
+// and a group's 12 quads are 12 KB in a row (the per-coefficient planes of 6.1M splats spread a
+// wave's 48 loads over 48 DRAM pages: 3.1 TB/s).
+__device__ __forceinline__ float4 sh_quad(const float *sh, size_t i, int q) {
+    return reinterpret_cast<const float4 *>(sh)[((i >> 6) * 12 + (size_t)q) * 64 + (i & 63)];
+}
 __device__ __forceinline__ float sh_channel(const float *sh, size_t n, size_t i, int c, float x, float y, float z) {
-    const float *p = sh + (size_t)(16 * c) * n + i;  // plane 16c + j holds coefficient j of channel c
+    (void)n;
     float k[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) k[j] = p[(size_t)j * n];
+    for (int q = 0; q < 4; ++q) {
+        const float4 v = sh_quad(sh, i, 4 * c + q);
+        k[4 * q] = v.x, k[4 * q + 1] = v.y, k[4 * q + 2] = v.z, k[4 * q + 3] = v.w;
+    }
     return sh_channel_k(k, x, y, z);
 }
 
 // The SH colours of a frame's splats with entries (GS_FLAG_SH), after k_preprocess (its emission
 // records say which): one splat per lane, all 48 coefficient loads issued before the arithmetic
-// (coalesced planes, ~9 KB in flight per wave) -- in the preprocess they came after its own
+// (12 coalesced 1-KB quad loads per wave, sh_quad) -- in the preprocess they came after its own
 // loads and math, under its register budget, in several round trips per item.
+#ifndef GS_SH_WAVES
+#define GS_SH_WAVES 4
+#endif
 template <bool PACK>
-__global__ __launch_bounds__(kBlock) void k_sh_colour(PreParams P, SceneDev sc, FrameDev fr) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(GS_SH_WAVES))) void k_sh_colour(PreParams P, SceneDev sc, FrameDev fr) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= P.n) return;
     const bool has = PACK ? (reinterpret_cast<const uint2 *>(fr.rec)[i].y >> 31) != 0 : fr.rec[i].y >= 0;
     if (!has) return;
-    const size_t n = (size_t)P.n;
     float k[48];
+    float4 v[12];
 #pragma unroll
-    for (int j = 0; j < 48; ++j) k[j] = sc.sh[(size_t)j * n + i];
-    float dx = sc.mx[i] - P.campos[0], dy = sc.my[i] - P.campos[1], dz = sc.mz[i] - P.campos[2];
+    for (int q = 0; q < 12; ++q) v[q] = sh_quad(sc.sh, (size_t)i, q);
+    float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
+    // all fifteen loads in flight before any arithmetic (left alone, the compiler split them into
+    // batches behind waits: three or four memory round trips per wave)
+#pragma unroll
+    for (int q = 0; q < 12; ++q) asm volatile("" : "+v"(v[q].x), "+v"(v[q].y), "+v"(v[q].z), "+v"(v[q].w));
+    asm volatile("" : "+v"(mx), "+v"(my), "+v"(mz));
+#pragma unroll
+    for (int q = 0; q < 12; ++q) k[4 * q] = v[q].x, k[4 * q + 1] = v[q].y, k[4 * q + 2] = v[q].z, k[4 * q + 3] = v[q].w;
+    float dx = mx - P.campos[0], dy = my - P.campos[1], dz = mz - P.campos[2];
     const float len = sqrtf(dx * dx + dy * dy + dz * dz);
     dx = dx / len;
     dy = dy / len;
