@@ -173,7 +173,7 @@ struct gs_scene {
     int n = 0;
     float *soa = nullptr;       // mx | my | mz | cov0..cov5 | opacity  (10 planes of n floats)
     float4 *colour = nullptr;   // (r,g,b,1)
-    float *sh = nullptr;        // GS_FLAG_SH: 48 coefficients per splat in 64-splat quad-major groups (sh_quad)
+    float *sh = nullptr;        // GS_FLAG_SH: 48 coefficients per splat, splat-major (sh_quad)
 };
 
 namespace gs {
@@ -822,11 +822,9 @@ int gs_scene_set_sh(gs_scene *scene, const float *f_dc3, const float *f_rest45) 
     if (int rc = use_device(ctx)) return rc;
     if (int rc = gs_sync(ctx)) return rc;  // frames in flight may read the old planes
     const size_t n = (size_t)scene->n;
-    // groups of 64 splats, quad-major within a group (gs_render.hip sh_quad): coefficient
-    // j = 16c + k of splat i at float ((i / 64 * 12 + j / 4) * 64 + i % 64) * 4 + j % 4
-    const size_t groups = std::max<size_t>((n + 63) / 64, 1);
-    std::vector<float> planes(groups * 64 * 48, 0.0f);
-    auto at = [](size_t i, int j) { return ((i / 64 * 12 + (size_t)(j / 4)) * 64 + i % 64) * 4 + (size_t)(j % 4); };
+    // splat-major (gs_render.hip sh_quad): coefficient j = 16c + k of splat i at float 48 i + j
+    std::vector<float> planes(48 * std::max<size_t>(n, 1), 0.0f);
+    auto at = [](size_t i, int j) { return i * 48 + (size_t)j; };
     for (size_t i = 0; i < n; ++i)
         for (int c = 0; c < 3; ++c) {
             planes[at(i, 16 * c)] = f_dc3[3 * i + c];

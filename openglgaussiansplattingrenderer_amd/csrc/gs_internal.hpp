@@ -196,7 +196,7 @@ struct SceneDev {
     const float *cov;            // 6 SoA planes of n floats: [S00 | S01 | S02 | S11 | S12 | S22]
     const float *opacity;
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
-    const float *sh;             // degree-3 SH, 64-splat groups of 12 coefficient quads (gs_render.hip sh_quad) or null
+    const float *sh;             // degree-3 SH, 48 floats per splat, splat-major (gs_render.hip sh_quad), or null
 };
 // per-splat blend inputs, 24 bytes (the blend gathers it with the colour; the pre-exp skip
 // threshold is derived from o where the blend needs it, draw_threshold)
