@@ -171,7 +171,7 @@ struct gs_ctx {
 struct gs_scene {
     gs_ctx *ctx = nullptr;
     int n = 0;
-    float *soa = nullptr;       // mx | my | mz | cov0..cov5 | opacity  (10 planes of n floats)
+    float *soa = nullptr;       // mx | my | mz planes, then the 32-byte shape records (gs::SceneDev)
     float4 *colour = nullptr;   // (r,g,b,1)
     float *sh = nullptr;        // GS_FLAG_SH: 48 coefficients per splat, splat-major (sh_quad)
 };
@@ -308,8 +308,7 @@ gs::SceneDev scene_dev(const gs_scene *s) {
     d.mx = s->soa;
     d.my = s->soa + n;
     d.mz = s->soa + 2 * n;
-    d.cov = s->soa + 3 * n;
-    d.opacity = s->soa + 9 * n;
+    d.shape = reinterpret_cast<const float4 *>(s->soa + gs::scene_shape_offset(n));
     d.colour = s->colour;
     d.sh = s->sh;
     return d;
@@ -671,13 +670,14 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
     if (int rc = use_device(ctx)) return rc;
     // host AoS (reference layout) -> device SoA planes
     const size_t nn = (size_t)n;
-    std::vector<float> soa(10 * std::max<size_t>(nn, 1));
+    std::vector<float> soa(std::max<size_t>(gs::scene_floats(nn), 1), 0.0f);
+    float *shape = soa.data() + gs::scene_shape_offset(nn);
     for (size_t i = 0; i < nn; ++i) {
         soa[i] = means4[4 * i + 0];
         soa[nn + i] = means4[4 * i + 1];
         soa[2 * nn + i] = means4[4 * i + 2];
-        for (int c = 0; c < 6; ++c) soa[(3 + c) * nn + i] = cov6[6 * i + c];
-        soa[9 * nn + i] = opacity[i];
+        for (int c = 0; c < 6; ++c) shape[8 * i + c] = cov6[6 * i + c];
+        shape[8 * i + 6] = opacity[i];
     }
     gs_scene *s = new gs_scene();
     s->ctx = ctx;
@@ -761,7 +761,7 @@ int gs_scene_load_ply(gs_ctx *ctx, const char *path, gs_scene **out) {
         }
         return GS_OK;
     };
-    if (hipMalloc(&s->soa, 10 * std::max<size_t>(nn, 1) * 4) != hipSuccess ||
+    if (hipMalloc(&s->soa, std::max<size_t>(gs::scene_floats(nn), 1) * 4) != hipSuccess ||
         hipMalloc(&s->colour, std::max<size_t>(nn, 1) * sizeof(float4)) != hipSuccess)
         return cleanup(GS_ERR_NOMEM, "gs_scene_load_ply: out of device memory");
     const size_t chunk = std::min(kChunk, std::max<size_t>(nn, 1));
@@ -796,7 +796,8 @@ int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *
     gs_ctx *ctx = scene->ctx;
     if (int rc = use_device(ctx)) return rc;
     const size_t nn = (size_t)scene->n;
-    std::vector<float> soa(10 * nn);
+    std::vector<float> soa(gs::scene_floats(nn));
+    const float *shape = soa.data() + gs::scene_shape_offset(nn);
     if (nn) GS_HIP(ctx, hipMemcpyAsync(soa.data(), scene->soa, soa.size() * 4, hipMemcpyDeviceToHost, ctx->L->stream));
     if (nn && colours4)
         GS_HIP(ctx, hipMemcpyAsync(colours4, scene->colour, nn * sizeof(float4), hipMemcpyDeviceToHost, ctx->L->stream));
@@ -809,8 +810,8 @@ int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *
             means4[4 * i + 3] = 1.f;
         }
         if (cov6)
-            for (int c = 0; c < 6; ++c) cov6[6 * i + c] = soa[(3 + c) * nn + i];
-        if (opacity) opacity[i] = soa[9 * nn + i];
+            for (int c = 0; c < 6; ++c) cov6[6 * i + c] = shape[8 * i + c];
+        if (opacity) opacity[i] = shape[8 * i + 6];
     }
     return GS_OK;
 }
@@ -890,7 +891,10 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 
 // covariance loads only for the splats inside the NDC square when the newest frame seen had most
 // of the scene's splats culled (the small C5 views)
-bool lazy_loads(const gs_ctx *ctx, int n) { return ctx->n == n && ctx->e_known && ctx->V * 2 < (int64_t)n; }
+#ifndef GS_QUEUE_FRAC
+#define GS_QUEUE_FRAC 2  // the queued preprocess when fewer than n / GS_QUEUE_FRAC splats were visible
+#endif
+bool lazy_loads(const gs_ctx *ctx, int n) { return ctx->n == n && ctx->e_known && ctx->V * GS_QUEUE_FRAC < (int64_t)n; }
 
 // preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->L->totals
 int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {

@@ -190,11 +190,16 @@ void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, 
                         hipEvent_t start = nullptr);
 
 // render kernels (gs_render.hip)
+// The scene on the device (gs_scene::soa): the means as three planes of n floats (the
+// projection reads them for every splat), then from scene_shape_offset(n) floats on one 32-byte
+// shape record per splat, (S00, S01, S02, S11) (S12, S22, opacity, 0): two 16-byte loads, which
+// lanes of NDC-culled splats can skip whole (k_preprocess_q, LAZY), instead of seven planes
+__host__ __device__ inline size_t scene_shape_offset(size_t n) { return (3 * n + 3) & ~(size_t)3; }
+__host__ __device__ inline size_t scene_floats(size_t n) { return scene_shape_offset(n) + 8 * n; }
 struct SceneDev {
     int n;
     const float *mx, *my, *mz;   // SoA means
-    const float *cov;            // 6 SoA planes of n floats: [S00 | S01 | S02 | S11 | S12 | S22]
-    const float *opacity;
+    const float4 *shape;         // [2 n]: (S00, S01, S02, S11), (S12, S22, opacity, 0) per splat
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
     const float *sh;             // degree-3 SH, 48 floats per splat, splat-major (gs_render.hip sh_quad), or null
 };
@@ -255,7 +260,7 @@ void launch_bins(hipStream_t s, const uint32_t *keys, int64_t E, const uint32_t 
 // GPU load path (gs_load.hip): count raw 62-float ply records starting at splat `base` ->
 // the scene's SoA planes (n floats each: mx my mz cov0..5 opacity) and colours
 constexpr int kPlyFloats = 62;
-void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, int n, float *soa, float4 *colour);
+void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, int n, float *soa, float4 *colour);  // soa: SceneDev layout
 
 // GS_FLAG_DRAW_STATS buffer: per block (launch order) kDrawTraceWords uint32: start, end
 // (s_memrealtime, 100 MHz), steps, survivors, (wave, survivor) steps, steps with a needing

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void k_ply_activate(const float *__restrict__ 
     colour[i] = make_float4((0.5f + (SH_C0 * r[6])) * 255.f, (0.5f + (SH_C0 * r[7])) * 255.f,
                             (0.5f + (SH_C0 * r[8])) * 255.f, 1.f);
     // :314-316 opacity = sigmoid(logit)
-    soa[9 * nn + i] = (1 / (1 + glibc_expf(-r[54])));
+    const float opac = (1 / (1 + glibc_expf(-r[54])));
     // :318-326 scale = exp(log scale); :328-331 rotation normalised
     const float sx = glibc_expf(r[55]), sy = glibc_expf(r[56]), sz = glibc_expf(r[57]);
     const float q0 = r[58], q1 = r[59], q2 = r[60], q3 = r[61];
@@ -49,12 +49,10 @@ __global__ __launch_bounds__(256) void k_ply_activate(const float *__restrict__ 
     for (int c = 0; c < 3; ++c)
 #pragma unroll
         for (int q = 0; q < 3; ++q) Sig[c][q] = M[q][0] * M[c][0] + M[q][1] * M[c][1] + M[q][2] * M[c][2];
-    soa[3 * nn + i] = Sig[0][0];
-    soa[4 * nn + i] = Sig[0][1];
-    soa[5 * nn + i] = Sig[0][2];
-    soa[6 * nn + i] = Sig[1][1];
-    soa[7 * nn + i] = Sig[1][2];
-    soa[8 * nn + i] = Sig[2][2];
+    // the shape record (SceneDev): covariance upper triangle and opacity
+    float4 *shape = reinterpret_cast<float4 *>(soa + scene_shape_offset(nn)) + 2 * i;
+    shape[0] = make_float4(Sig[0][0], Sig[0][1], Sig[0][2], Sig[1][1]);
+    shape[1] = make_float4(Sig[1][2], Sig[2][2], opac, 0.0f);
 }
 
 }  // namespace

@@ -286,13 +286,11 @@ template <bool CLEAN, bool LAZY>
 __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDev &sc, const FrameDev &fr, int i,
                                                bool valid) {
     if (!valid) return make_int4(0, -1, -1, 0);
-    const size_t n = (size_t)P.n;
     const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
     float c0, c1, c2, c3, c4, c5, opac;
-    if (!LAZY) {  // all ten planes in one round trip (see LAZY)
-        c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
-        c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
-        opac = sc.opacity[i];
+    if (!LAZY) {  // the means and the shape record in one round trip (see LAZY)
+        const float4 s0 = sc.shape[2 * (size_t)i], s1 = sc.shape[2 * (size_t)i + 1];
+        c0 = s0.x, c1 = s0.y, c2 = s0.z, c3 = s0.w, c4 = s1.x, c5 = s1.y, opac = s1.z;
     }
     // Straight-line body: every cull folds into `vis` and the outputs are selected at the
     // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
@@ -303,9 +301,8 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
     if (LAZY) {
         c0 = c1 = c2 = c3 = c4 = c5 = opac = 0.0f;
         if (vis) {
-            c0 = sc.cov[i], c1 = sc.cov[n + i], c2 = sc.cov[2 * n + i];
-            c3 = sc.cov[3 * n + i], c4 = sc.cov[4 * n + i], c5 = sc.cov[5 * n + i];
-            opac = sc.opacity[i];
+            const float4 s0 = sc.shape[2 * (size_t)i], s1 = sc.shape[2 * (size_t)i + 1];
+            c0 = s0.x, c1 = s0.y, c2 = s0.z, c3 = s0.w, c4 = s1.x, c5 = s1.y, opac = s1.z;
         }
     }
     return preprocess_rest<CLEAN>(P, sc, fr, i, mx, my, mz, p0, p1, p2, vis, c0, c1, c2, c3, c4, c5, opac);
@@ -481,7 +478,6 @@ template <bool PACK, bool CLEAN>
 __global__ __launch_bounds__(64 * kQWaves) void k_preprocess_q(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_sum[kQWaves];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const size_t n = (size_t)P.n;
     const int base = blockIdx.x * kSplatsPerBlock + wid * (kQItems * 64);
     uint32_t n_main = 0, n_dup = 0;
     // queue: entries [0, qn) in lanes of qa (the first 64) and qb (the overflow)
@@ -552,9 +548,8 @@ __global__ __launch_bounds__(64 * kQWaves) void k_preprocess_q(PreParams P, Scen
             pi = qa_i, pp0 = qa0, pp1 = qa1, pp2 = qa2;
             if (lane < pend_n) {
                 pmx = sc.mx[pi], pmy = sc.my[pi], pmz = sc.mz[pi];
-                pc0 = sc.cov[pi], pc1 = sc.cov[n + pi], pc2 = sc.cov[2 * n + pi];
-                pc3 = sc.cov[3 * n + pi], pc4 = sc.cov[4 * n + pi], pc5 = sc.cov[5 * n + pi];
-                pop = sc.opacity[pi];
+                const float4 s0 = sc.shape[2 * (size_t)pi], s1 = sc.shape[2 * (size_t)pi + 1];
+                pc0 = s0.x, pc1 = s0.y, pc2 = s0.z, pc3 = s0.w, pc4 = s1.x, pc5 = s1.y, pop = s1.z;
             }
             qa_i = qb_i, qa0 = qb0, qa1 = qb1, qa2 = qb2;
             qn -= pend_n;
