@@ -728,6 +728,10 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
     const uint32_t tile = blockIdx.x;
+    if (BKT && live == 0 && tile == 0) {  // no keys: every bucket empty (k_bucket_sort reads the table)
+        bkt[threadIdx.x] = 0u;
+        bkt[kRadix + threadIdx.x] = 0u;
+    }
     if (tile >= live) return;  // uniform
     __shared__ uint32_t s_cnt[kWaves][kRadix];
     __shared__ uint32_t s_start[kRadix];
@@ -1144,9 +1148,11 @@ int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, boo
         }
         sc.hist_cap = cap;
     }
-    if (!sc.bkt && hipMalloc(&sc.bkt, 2 * kRadix * 4) != hipSuccess) {  // the bucket form's (base, count) table
-        err = "radix sort: out of device memory";
-        return GS_ERR_NOMEM;
+    if (!sc.bkt) {  // the bucket form's (base, count) table, zeroed: a sort of no keys reads it as empty
+        if (hipMalloc(&sc.bkt, 2 * kRadix * 4) != hipSuccess || hipMemsetAsync(sc.bkt, 0, 2 * kRadix * 4, s) != hipSuccess) {
+            err = "radix sort: out of device memory";
+            return GS_ERR_NOMEM;
+        }
     }
     if (!sc.row_total) {  // row totals [256] + tile counts [16][256] + above-1e6 counts [16] (zero between sorts)
         const size_t bytes = ((size_t)(1 + kTileCopies) * kRadix + kTileCopies) * 4;
