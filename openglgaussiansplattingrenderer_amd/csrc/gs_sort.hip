@@ -975,7 +975,7 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
                                                                uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                                const uint32_t *__restrict__ bkt,
                                                                uint32_t *__restrict__ tile_counts,
-                                                               uint32_t *__restrict__ bins) {
+                                                               uint32_t *__restrict__ bins, uint32_t cap) {
     static_assert(kWaveSmall * 64 == kRadix, "one thread per digit");
     constexpr uint32_t kTile = kTileSmall;
     if (bins && blockIdx.x == kRadix) {  // uniform: the bins workgroup
@@ -988,7 +988,9 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
     __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
     __shared__ uint32_t s_wave[kWaveSmall];
     __shared__ uint32_t s_mm[2][kWaveSmall];
-    const uint32_t b0 = bkt[blockIdx.x], m = bkt[kRadix + blockIdx.x];
+    // (the table is the sweep's; a bucket is still held inside the arrays' n = cap entries, so a
+    // table that is not this sort's can misorder a frame but never reach past its arrays)
+    const uint32_t b0 = bkt[blockIdx.x], m = min(bkt[kRadix + blockIdx.x], cap - min(b0, cap));
     if (m == 0) return;  // uniform
     // (uniform) short buckets with 4 keys per lane, up to 4096 with 16
     if (m <= kTile / 4) return bucket_fast<kItems / 4>(kin, vin, kout, vout, b0, m, s_k, s_v, s_cnt, s_start, s_wave, s_tdig, s_mm);
@@ -1236,7 +1238,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
                                   pass == 0 && !bk ? bins : nullptr, sc.bkt);
             if (bk) {  // (alt -> keys: the result is where the 4-pass form leaves it)
                 hipExtLaunchKernelGGL(k_bucket_sort, dim3(kRadix + (bins ? 1 : 0)), dim3(kWaveSmall * 64), 0, s, nullptr, stop, 0,
-                                      kout, vout, kin, vin, sc.bkt, tile_counts, bins);
+                                      kout, vout, kin, vin, sc.bkt, tile_counts, bins, (uint32_t)n);
                 break;
             }
             std::swap(kin, kout);
