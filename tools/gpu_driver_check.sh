@@ -4,7 +4,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
-timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $O/dc_tests.log 2>&1 || { echo TESTS_FAIL; tail -5 $O/dc_tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > $O/dc_tests.log 2>&1 || { echo TESTS_FAIL; tail -5 $O/dc_tests.log; exit 1; }
 tail -1 $O/dc_tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/dc_smoke.log 2>&1 || { echo SMOKE_FAIL; tail -5 $O/dc_smoke.log; exit 1; }
 tail -1 $O/dc_smoke.log
