@@ -204,7 +204,11 @@ def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
         if i >= warm:
             ms.append(t)
     k_out = kb.download(np.uint32, n)
-    ok = bool(np.all(k_out[1:] >= k_out[:-1]))
+    v_out = vb.download(np.uint32, n)
+    # sorted, and the values a stable permutation carrying each key (vals were 0..n-1)
+    ok = bool(np.all(k_out[1:] >= k_out[:-1]) and np.all(v_out < n)
+              and np.array_equal(keys[np.minimum(v_out, n - 1)], k_out)
+              and np.all((k_out[1:] != k_out[:-1]) | (v_out[1:] > v_out[:-1])))
     med = float(np.median(ms))
     b_counter = 83.4  # B/key, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this sort (profiles/r03/sort_64M.txt)
     return dict(n=n, keys="uniform 32-bit, seeded", ms_pairs=round(med, 4), gkeys_per_s=round(n / med / 1e6, 2),

@@ -137,6 +137,13 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t live) {
     const uint32_t per = (live + 7) / 8, j = blockIdx.x >> 3;
     return j < per ? (blockIdx.x & 7u) * per + j : 0xffffffffu;  // (>= live: no tile)
 }
+// the same ranges walked from their ends: a pass's upsweep over a key array larger than the
+// 256 MiB Infinity Cache, walked backwards, leaves the first tiles of each range -- where its
+// downsweep starts -- the most recently read, so those key lines are still cached there
+__device__ __forceinline__ uint32_t xcd_tile_rev(uint32_t live) {
+    const uint32_t per = (live + 7) / 8, j = blockIdx.x >> 3;
+    return j < per ? (blockIdx.x & 7u) * per + (per - 1 - j) : 0xffffffffu;
+}
 __host__ __device__ constexpr uint32_t xcd_grid(uint32_t nb) { return 8 * ((nb + 7) / 8); }
 
 // W waves per workgroup, tile = W * 1024 keys (the pass-0 sort uses W = 8: its random low
@@ -166,7 +173,7 @@ __device__ __forceinline__ uint32_t digit_of(uint32_t key, int shift) {
     return BKT ? bucket_of(key) : (key >> shift) & 0xffu;
 }
 
-template <int W, bool TILES, bool PREFIX = false, bool BKT = false, int IT = kItems>
+template <int W, bool TILES, bool PREFIX = false, bool BKT = false, int IT = kItems, bool REV = false>
 __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__ keys, uint32_t n_max,
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     static_assert(kThreads >= kRadix, "one thread per digit flushes the counts");
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
-    const uint32_t tile = xcd_tile(live);
+    const uint32_t tile = REV ? xcd_tile_rev(live) : xcd_tile(live);
     if (tile >= live) return;  // uniform: tile beyond the count (never scanned)
     // counts need no ranks: LDS atomics.  Each digit has kRep counters picked by lane % 8, so
     // a wave whose keys share one digit (the top-byte pass) serialises 8-way, not 64-way.
@@ -1263,6 +1270,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     // ~2M, ran 3 % slower that way; 12- and 16-wave tiles spill: 2.8 / 3.5 ms against 1.20)
     // (standalone pair sorts: no bins, pairs out in every pass)
     const bool all_big = !pre && !bins && keys_out && n >= (int64_t)1 << 24;
+#ifndef GS_UPSWEEP_REV
+#define GS_UPSWEEP_REV 1
+#endif
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
         const bool big = pass == 0 || all_big;
@@ -1281,6 +1291,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         else if (big && bins)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
                                   kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split, nullptr);
+        else if (big && all_big && GS_UPSWEEP_REV)  // (standalone sorts of >= 16M keys)
+            hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false, false, false, kItems, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64),
+                                  0, s, e0, nullptr, 0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split, nullptr);
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
                                   kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split, nullptr);

@@ -89,3 +89,24 @@ def test_sort_pairs_distributions(ctx, dist):
     o = np.argsort(k, kind="stable")
     assert np.array_equal(ks, k[o])
     assert np.array_equal(vs, v[o])
+
+
+@pytest.mark.parametrize("dist", ["uniform32", "top_byte_const"])
+def test_sort_pairs_beyond_16M(ctx, dist):
+    """standalone pair sorts of >= 16M keys take the 8-wave form in every pass, with the upsweeps
+    walking each XCD's tile range backwards (k_upsweep REV): a ragged size past 2^24, bit-exact
+    stable pairs"""
+    import openglgaussiansplattingrenderer_amd as g
+    rng = np.random.default_rng(24)
+    n = (1 << 24) + 12_345
+    if dist == "uniform32":
+        k = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    else:
+        k = (0x42000000 | rng.integers(0, 2**24, n)).astype(np.uint32)
+    v = np.arange(n, dtype=np.uint32)
+    kb, vb = g.DeviceBuffer.from_array(ctx, k), g.DeviceBuffer.from_array(ctx, v)
+    g.sort_pairs(ctx, kb, vb, n)
+    ks, vs = kb.download(np.uint32, n), vb.download(np.uint32, n)
+    o = np.argsort(k, kind="stable")
+    assert np.array_equal(ks, k[o])
+    assert np.array_equal(vs, o.astype(np.uint32))
