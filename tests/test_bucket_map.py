@@ -33,3 +33,41 @@ def test_bucket_of_is_monotone_in_the_key_bits():
     # and each tile's keys [t, t + 1) land in bucket t
     ok = (z >= 0) & (z < 1) & ((tiles + z) < tiles + 1)
     assert np.array_equal(bucket_of((tiles + z).view(np.uint32))[ok], tiles[ok].astype(np.int64))
+
+
+def bucket_form(keys: np.ndarray, vals: np.ndarray):
+    """numpy restatement of the bucket form (gs_sort.hip k_sweep_small<BKT> + k_bucket_sort):
+    stable scatter by bucket_of, then per bucket the 8-bit LSD passes over the bits below the
+    highest one where its smallest and largest key differ (bucket_passes)"""
+    b = bucket_of(keys)
+    o = np.argsort(b, kind="stable")
+    k, v, b = keys[o], vals[o], b[o]
+    for d in np.unique(b):
+        idx = np.nonzero(b == d)[0]
+        kk, vv = k[idx], v[idx]
+        diff = int(kk.min()) ^ int(kk.max())
+        passes = (diff.bit_length() + 7) // 8
+        for p in range(passes):
+            oo = np.argsort((kk >> np.uint32(8 * p)) & np.uint32(0xFF), kind="stable")
+            kk, vv = kk[oo], vv[oo]
+        k[idx], v[idx] = kk, vv
+    return k, v
+
+
+def test_bucket_form_is_the_stable_sort_of_ref_mode_keys():
+    """the withdrawn GPU scene's key kinds (NDC depths -1.5..2.5 in ref mode: keys below their
+    tile, negative floats for tile 0, keys past tile + 1), the culled 1e6 entries and ties: the
+    bucket form's order is the stable sort by the unsigned key bits"""
+    rng = np.random.default_rng(7)
+    n = 60_000
+    tiles = rng.integers(0, 256, n).astype(np.float32)
+    tiles[: n // 8] = 0.0  # tile 0: depths below 0 give negative floats (bucket 255)
+    z = rng.uniform(-1.5, 2.5, n).astype(np.float32)
+    keys = (tiles + z).view(np.uint32).copy()
+    keys[rng.random(n) < 0.05] = 0x49742400  # culled entries: 1e6
+    keys[rng.random(n) < 0.05] = keys[0]     # ties
+    vals = np.arange(n, dtype=np.uint32)
+    k, v = bucket_form(keys, vals)
+    o = np.argsort(keys, kind="stable")
+    assert np.array_equal(k, keys[o])
+    assert np.array_equal(v, vals[o])
