@@ -286,9 +286,9 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
 // draw's tile order bins[256 + r] = the tile with the r-th longest list (ties by index); the
 // counts are cleared for the next frame
 // (returns the tile's count and the exclusive prefix; *s_above gets the keys above 1e6)
+// (s_c: kRadix words of LDS, 16-byte aligned, the caller's)
 __device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, uint32_t *s_w,
-                           uint32_t *s_above) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_c[kRadix];
+                           uint32_t *s_above, uint32_t *s_c) {
     const int t = threadIdx.x;
     uint32_t v = 0;
 #pragma unroll
@@ -320,7 +320,9 @@ __device__ uint2 bins_scan(uint32_t *__restrict__ counts, uint32_t *__restrict__
         __syncthreads();
         const uint32_t key = (v << 8) | (uint32_t)(255 - t);
         const uint4 *q = reinterpret_cast<const uint4 *>(s_c);
-#pragma unroll 16
+        // (unrolled by 4, not 16: 16 VGPRs of reads in flight, so the kernels holding this
+        // workgroup stay within the 64 VGPRs a SIMD has free beside seven blend waves)
+#pragma unroll 4
         for (int u = 0; u < kRadix / 4; ++u) {
             const uint4 c = q[u];
             r += (c.x > key ? 1u : 0u) + (c.y > key ? 1u : 0u) + (c.z > key ? 1u : 0u) + (c.w > key ? 1u : 0u);
@@ -392,21 +394,24 @@ __device__ void prefix_counts(const uint32_t *__restrict__ tile_counts, const Pr
 // the first position of its draw window that was not sorted -- in the draw's positions, which
 // hold the reference's culled entries (cn of them at cpos, k_draw) besides the sorted ones;
 // 0xffffffff: none.
+// LDS: s_PG holds bins_scan's scratch, then the class starts s_P and the gaps s_G (2 KB in all:
+// with the row scans' 16 B this workgroup's kernel fits beside seven blend waves per SIMD); the
+// kept ends are read from pre.cls where the search lands
 __device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restrict__ bins, const PrefixDev &pre,
-                              const uint32_t *__restrict__ cnt, uint32_t *s_w) {
+                              const uint32_t *__restrict__ cnt, uint32_t *s_w, uint32_t *s_PG) {
     __shared__ uint32_t s_above;
-    __shared__ uint32_t s_P[kClasses + 1], s_L[kClasses], s_G[kClasses], s_gw[4];
+    __shared__ uint32_t s_gw[4];
+    uint32_t *s_P = s_PG, *s_G = s_PG + (kClasses + 1);
     const int t = threadIdx.x, lane = lane_id(), wid = t >> 6;
-    const uint2 vb = bins_scan(counts, bins, s_w, &s_above);  // (its barriers publish s_above)
+    const uint2 vb = bins_scan(counts, bins, s_w, &s_above, s_PG);  // (its barriers publish s_above)
     const uint32_t P = pre.cls[t], L = pre.cls[kClasses + 1 + t];
     const uint32_t P256 = pre.cls[256], E = pre.cls[257], L256 = pre.cls[kClasses + 1 + 256];
     const uint32_t Pn = t < 255 ? pre.cls[t + 1] : P256;  // the next class's start
+    __syncthreads();  // every thread's bins_scan reads of s_PG are done
     s_P[t] = P;
-    s_L[t] = L;
     if (t == 0) {
         s_P[256] = P256;
         s_P[257] = E;
-        s_L[256] = L256;
     }
     // G[c]: the first position not sorted at or after class c's start (E: none) -- a suffix min
     // of each class's gap (its kept end, when it kept less than all)
@@ -438,7 +443,7 @@ __device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restric
 #pragma unroll
         for (int step = 256; step > 0; step >>= 1)
             if (c + step <= 256 && s_P[c + step] <= q0) c += step;
-        const uint32_t fq = q0 >= s_L[c] ? q0 : s_G[c];
+        const uint32_t fq = q0 >= pre.cls[kClasses + 1 + c] ? q0 : s_G[c];
         if (fq < E) fi = fq < cpos ? fq : fq + cn;
     }
     bins[kBinsLimit + t] = fi;
@@ -454,19 +459,20 @@ __device__ void prefix_limits(uint32_t *__restrict__ counts, uint32_t *__restric
 // BINS false (a pass without the bins workgroup): none of its LDS and a few VGPRs -- 16 bytes
 // of LDS and kPer 4 fit beside seven blend waves per SIMD, so another frame's blend leaves room
 template <int kPer = 16, bool BINS = true>
-__global__ __launch_bounds__(256) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 ? 8 : 1))) void k_scan_rows(uint32_t *__restrict__ hist, uint32_t nb_stride, uint32_t n_max,
                                                    const uint32_t *__restrict__ cnt, uint32_t tile,
                                                    uint32_t *__restrict__ row_total, uint32_t *__restrict__ tile_counts,
                                                    uint32_t *__restrict__ bins, PrefixDev pre, int prefix) {
     __shared__ uint32_t s_w[4];
     if (BINS && blockIdx.x == kRadix) {  // uniform: the bins workgroup
+        __shared__ __attribute__((aligned(16))) uint32_t s_PG[2 * (kClasses + 1) + 1];
         if (prefix == 1) {
             prefix_counts(tile_counts, pre, cnt, n_max, s_w);
         } else if (prefix == 2) {
-            prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w);
+            prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w, s_PG);
         } else {
             __shared__ uint32_t s_above;
-            bins_scan(tile_counts, bins, s_w, &s_above);
+            bins_scan(tile_counts, bins, s_w, &s_above, s_PG);
         }
         return;
     }
@@ -729,7 +735,8 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_sweep_small(const uint32_t 
     __shared__ uint32_t s_w[4];
     if (bins && blockIdx.x == gridDim.x - 1) {  // uniform: the bins workgroup (first pass)
         __shared__ uint32_t s_above;
-        bins_scan(tile_counts, bins, s_w, &s_above);
+        __shared__ __attribute__((aligned(16))) uint32_t s_c[kRadix];
+        bins_scan(tile_counts, bins, s_w, &s_above, s_c);
         return;
     }
     const uint32_t n = elem_count(n_max, cnt);
@@ -987,7 +994,8 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
     constexpr uint32_t kTile = kTileSmall;
     if (bins && blockIdx.x == kRadix) {  // uniform: the bins workgroup
         __shared__ uint32_t s_w[4], s_above;
-        bins_scan(tile_counts, bins, s_w, &s_above);
+        __shared__ __attribute__((aligned(16))) uint32_t s_c[kRadix];
+        bins_scan(tile_counts, bins, s_w, &s_above, s_c);
         return;
     }
     __shared__ uint32_t s_k[kTile], s_v[kTile];
@@ -1307,7 +1315,12 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
 #ifndef GS_SCAN_LIGHT
 #define GS_SCAN_LIGHT 1
 #endif
-        auto scan = with_bins ? (nb > 4096 ? k_scan_rows<64> : k_scan_rows<16>)
+#ifndef GS_SCAN_LIGHT_BINS
+#define GS_SCAN_LIGHT_BINS 1
+#endif
+        // (the passes with the bins workgroup in the light form too: 4 counts per thread, and the
+        // bins workgroup's LDS shared between its phases -- ~2 KB in all)
+        auto scan = with_bins ? (nb > 4096 ? k_scan_rows<64> : GS_SCAN_LIGHT_BINS ? k_scan_rows<4> : k_scan_rows<16>)
                     : nb > 4096  ? k_scan_rows<64, false>
                     : (GS_SCAN_LIGHT && nb <= 1024) ? k_scan_rows<4, false>
                                                     : k_scan_rows<16, false>;
