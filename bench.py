@@ -219,6 +219,101 @@ def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
                        "counters (profiles/r03/sort_64M.txt)")
 
 
+def sort_bench_c3(ctx, sp, u, reps: int = 20, warm: int = 3):
+    """The reference's per-frame work on the C3 frame's own key set: every (key, value) pair the
+    frame emits, sorted in full (GPURadixSort orders all entries each frame, src/sort.cpp:139-203)
+    by the standalone pair sort (12 kernels, keys and values out).  The entries are the emission's
+    (the staged preprocess, before gs_sort: splat-major order, keys tile + z01)."""
+    import openglgaussiansplattingrenderer_amd as g
+    sp._preprocess_u(u)
+    E = int(sp.stats.entries)
+    keys = sp.read(g.GS_READ_KEYS, E)
+    vals = sp.read(g.GS_READ_VALS, E)
+    kb = g.DeviceBuffer.from_array(ctx, keys)
+    vb = g.DeviceBuffer.from_array(ctx, vals)
+    ms = []
+    for i in range(warm + reps):
+        kb.upload(keys)
+        vb.upload(vals)
+        g.sort_pairs(ctx, kb, vb, E)
+        t = ctx.last_kernel_ms(g.GS_KERNEL_SORT)
+        if i >= warm:
+            ms.append(t)
+    k_out = kb.download(np.uint32, E)
+    v_out = vb.download(np.uint32, E)
+    perm = np.argsort(keys, kind="stable")
+    ok = bool(np.array_equal(k_out, keys[perm]) and np.array_equal(v_out, vals[perm]))
+    med = float(np.median(ms))
+    del kb, vb
+    return dict(n=E, keys="the C3 frame's emitted (tile + depth) keys, splat ids as values", ms_pairs=round(med, 4),
+                gkeys_per_s=round(E / med / 1e6, 2),
+                hbm_frac_algorithmic=round(68.0 * E / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), sorted_ok=ok,
+                note="80 MB of pairs (160 MB with the alternate buffers): inside the 256 MiB Infinity Cache, so "
+                     "the rate is partly a cache figure",
+                source="hipEvents around gs_sort_pairs_u32 (12 kernels), median of %d; 68 B/key algorithmic" % reps)
+
+
+def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, static_fps: float,
+                 deltas=(0.5, 3.0)):
+    """The reference's loop moves the camera every frame (main.cpp:52-89 calls getInput at :76,
+    src/Camera.cpp:77-119).  Pose k = the static pose + rotateRight(delta * k): an interactive
+    (0.5 deg / frame) and a fast (3 deg / frame) pan, `steps` frames each on `lanes` frames in
+    flight, with the prefix sort (the per-tile depths carried from frame to frame) and with every
+    frame fully sorted; each run starts from a cold depth table, whose first frame is also timed
+    alone (one lane)."""
+    import openglgaussiansplattingrenderer_amd as g
+    base = ctx.set_sort_prefix()
+    out = {}
+    for d in deltas:
+        poses = []
+        for k in range(steps):
+            cam = camera_for_rank(W, H, view)
+            cam.rotateRight(d * k)
+            poses.append(cam.uniforms())
+        row = {"deg_per_frame": d, "frames": steps, "pan_deg": round(d * (steps - 1), 2)}
+        for mode, tgt in (("prefix", base), ("full_sort", 0)):
+            ctx.set_sort_prefix(tgt)  # (clears the per-tile depths: a cold start)
+            ctx.set_lanes(1)
+            ctx.sync()
+            t0 = time.perf_counter()
+            sp.render_uniforms(poses[0])
+            ctx.sync()
+            first_ms = (time.perf_counter() - t0) * 1e3
+            ctx.set_lanes(lanes)
+            ctx.prefix_stats(reset=True)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for uu in poses:
+                sp.render_uniforms(uu)
+            ctx.sync()
+            dt = time.perf_counter() - t0
+            ps = ctx.prefix_stats()
+            row[mode] = {"frames_per_s": round(steps / dt, 2), "vs_static": round(steps / dt / static_fps, 4),
+                         "cold_first_frame_ms": round(first_ms, 4),
+                         "prefix_frames": ps["frames"], "rendered_again": ps["redone"],
+                         "kept_frac_last": round(ps["kept"] / max(1, ps["entries"]), 4),
+                         "E_last": int(sp.stats.entries)}
+        out[f"{d:g}deg"] = row
+    ctx.set_sort_prefix(base)
+    out["source"] = ("host wall clock around the frames (gs_sync after the last); vs_static = frames/s over the "
+                     "static headline's value from the same run; cold_first_frame_ms: the first pose alone, one "
+                     "lane, host wall clock around gs_render + gs_sync")
+    return out
+
+
+def copy_peak(ctx, nbytes: int = 1 << 30, reps: int = 10):
+    """stream-copy rate of this GPU in this run (gs_stream_copy_gbs: float4 grid-stride copy of
+    1 GiB, read + write bytes): the practical HBM ceiling beside the 8 TB/s spec"""
+    import ctypes
+    from openglgaussiansplattingrenderer_amd import _native as native
+    med, best = ctypes.c_double(), ctypes.c_double()
+    native.check(native.lib().gs_stream_copy_gbs(ctx.handle, nbytes, reps, ctypes.byref(med), ctypes.byref(best)),
+                 ctx.handle)
+    return dict(gbs_median=round(med.value, 1), gbs_best=round(best.value, 1), bytes=nbytes, reps=reps,
+                source="gs_stream_copy_gbs: float4 grid-stride copy between two 1 GiB buffers, hipEvents, "
+                       "(read + write bytes) / time, median of %d" % reps)
+
+
 def cpu_baseline(sp, u, flags, budget_s: float = 20.0):
     """CPU oracle on the host cores, bounded: full preprocess + emit + sort + bins of the
     same frame, blend on every row_step-th pixel row (time scaled by row_step)."""
@@ -304,6 +399,7 @@ def main():
                     help="the blend's sub-block form (gs_ctx_set_draw_sub): 0 by entry count (default), 8, 16")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the moving-camera frames (frame.camera_sweep)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only (spawn / rendezvous / per-rank pose / barrier / gather), no GPU: "
@@ -476,9 +572,25 @@ def main():
         ranks = [None] * world
         pg.all_gather_object(ranks, mine)
 
+    sweep = None
+    if not args.no_sweep and args.config != "c2":
+        sweep = camera_sweep(ctx, sp, W, H, view, args.steps, args.lanes, value / world)
+    copy = copy_peak(ctx) if rank == 0 else None
+    if copy:
+        roofline["copy_peak_gbs"] = copy["gbs_median"]
+        roofline["frac_of_copy"] = round(roofline["achieved"] / copy["gbs_median"], 4)
+        roofline["copy_source"] = copy["source"]
     sort = None
     if not args.no_sort_bench and rank == 0:
         sort = sort_bench(ctx)
+        if args.config != "c2":
+            sort["c3_full"] = sort_bench_c3(ctx, sp, u)
+        if copy:
+            for k in ("beyond_cache", "c3_full"):
+                if k in sort:
+                    b = sort[k]
+                    b["frac_of_copy_algorithmic"] = round(68.0 * b["n"] / (b["ms_pairs"] * 1e-3) / 1e9 /
+                                                          copy["gbs_median"], 4)
     cpu = None
     if not args.no_cpu_baseline and rank == 0 and world == 1:
         cpu = cpu_baseline(sp, u, flags, budget_s=args.cpu_budget)
@@ -513,6 +625,7 @@ def main():
                       "serial_ms_per_frame": round(serial_ms, 4),
                       "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
                       "prefix_sort": prefix,
+                      "camera_sweep": sweep,
                       "frame_bytes_algorithmic": int(frame_bytes),
                       "frame_hbm_frac_algorithmic": round(frame_frac, 4),
                       "frame_bytes_source": "40N + 24V (preprocess) + 8E (emission) + sort (4E + 16E + 48 kept "

@@ -105,8 +105,9 @@ int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
  * an unsorted position before saturating is rendered again with the full sort, and the target
  * doubles for the frames after it; after 64 frames in a row without a miss it halves again,
  * never below the configured target.  target 0: always the full sort.  Frames with fewer than
- * 64 * target entries (the previous frame's count) use the full sort.  Returns the current
- * target in *current when it is not NULL (with target < 0: only that). */
+ * 64 * target entries (the previous frame's count) use the full sort.  Setting a target
+ * (>= 0) also clears the per-tile depths the blends recorded (a cold start).  Returns the
+ * current target in *current when it is not NULL (with target < 0: only that). */
 int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current);
 /* The blend's sub-block form (beyond the reference, whose draw.glsl runs 32x32 workgroups,
  * src/Splats.cpp:378): 16 = one wave per 16x16 pixels, each lane a 2x2 quad (throughput form:
@@ -123,6 +124,14 @@ int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entr
  * scatter by int(key), then LSD passes per tile in LDS); 0 = four 8-bit passes (8 launches);
  * -1 leaves it.  Returns the form now set (or a negative GS_ERR_*).  Same result either way. */
 int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on);
+/* The fused preprocess + emission of small scenes (<= 64k splats, frames enqueued without a host
+ * round trip) places each workgroup's entries by a decoupled look-back over the workgroups before
+ * it.  A wait for a predecessor is bounded (default 2^15 polls); a workgroup that gives up emits
+ * at partial offsets and flags the frame, which the host renders again on the host-synchronous
+ * path (same image).  limit 0 gives up at once (a test hook for that path); limit < 0 leaves it.
+ * Returns the limit now set; *redone (when not NULL) receives the number of frames rendered
+ * again for this reason. */
+int gs_ctx_set_lookback_spin(gs_ctx *ctx, int limit, uint64_t *redone);
 /* prefix-sort counters: [0] frames prefix-sorted, [1] of them rendered again (a blend reached
  * an unsorted position), [2] entries kept by the newest retired prefix-sorted frame, [3] its
  * entry count; reset != 0 clears [0] and [1] */
@@ -134,6 +143,11 @@ int gs_free(gs_ctx *ctx, void *dptr);
 int gs_memcpy_h2d(gs_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* measurement helper (bench.py's roofline.frac_of_copy; not on the frame path): the stream-copy
+ * rate of the ctx's GPU -- a float4 grid-stride copy of `bytes` between two fresh device buffers,
+ * read + written bytes per second, median (and best) of `reps` hipEvent-timed copies */
+int gs_stream_copy_gbs(gs_ctx *ctx, size_t bytes, int reps, double *gbs_median, double *gbs_best);
 
 /* ------------------------------------------------------- host: loader etc. */
 /* src/Splats.cpp:250-262: N from the header ("element vertex N" on line 3) */

@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstring>
 #include <iostream>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -153,17 +154,24 @@ inline int GPURadixSort(unsigned histogramProgram, unsigned prefixSumProgram, un
 // include/Splats.h:29-124
 class Splats {
   public:
-    // src/Splats.cpp:15-26: load the ply, compute the covariances on the host, upload.
+    // src/Splats.cpp:15-26 with the reference's arguments (include/Splats.h:33, main.cpp:47): the
+    // scene lives on the calling thread's current Context, as the reference's buffers live in the
+    // current GL context; with none current, the Splats creates one on device 0 (owned, current)
+    Splats(const std::string &filePath, int width, int height) : ctx_(Context::current()) {
+        if (!ctx_) {
+            own_.reset(new Context(0));
+            own_->makeCurrent();
+            ctx_ = own_.get();
+        }
+        setup(filePath, width, height);
+    }
+    // the same on an explicit Context (e.g. one per GPU from one thread), with render flags
     Splats(const std::string &filePath, int width, int height, Context &ctx, uint32_t flags = 0)
-        : ctx_(ctx), flags_(flags) {
-        std::cout << "setting up splats" << std::endl;
-        loadSplats(filePath);
-        computeCovarianceMatrices();
-        loadToGPU(width, height);
-        std::cout << "finished setting up splats" << std::endl;
+        : ctx_(&ctx), flags_(flags) {
+        setup(filePath, width, height);
     }
     ~Splats() {
-        if (texture_) gs_free(ctx_.get(), texture_);
+        if (texture_) gs_free(ctx_->get(), texture_);
         gs_scene_destroy(scene_);
     }
     Splats(const Splats &) = delete;
@@ -172,9 +180,9 @@ class Splats {
     void loadToGPU(int width, int height) {
         if (scene_) gs_scene_destroy(scene_);
         scene_ = nullptr;
-        report(gs_scene_create(ctx_.get(), numSplats, &means3D[0].x, covarianceMatrices.data(), opacities.data(),
+        report(gs_scene_create(ctx_->get(), numSplats, &means3D[0].x, covarianceMatrices.data(), opacities.data(),
                                &colours[0].x, &scene_),
-               ctx_.get());
+               ctx_->get());
         ensureTexture(width, height);
     }
     void loadShaders() {}  // src/Splats.cpp:156-172: nothing to compile at run time
@@ -185,7 +193,7 @@ class Splats {
         preprocess(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix);
         computeBins();
         sort();
-        ctx_.finish();
+        ctx_->finish();
         draw(width, height, float(width) / 16.f, float(height) / 16.f);
     }
     // src/Splats.cpp:542-585 (+ emission; the duplicate count is exact, not capped)
@@ -201,31 +209,31 @@ class Splats {
         u.tan_fov_x = tan_fov_x;
         u.tan_fov_y = tan_fov_y;
         gs_frame_stats st{};
-        report(gs_preprocess(ctx_.get(), scene_, &u, flags_, &st), ctx_.get());
+        report(gs_preprocess(ctx_->get(), scene_, &u, flags_, &st), ctx_->get());
         numDuplicates = (int)st.duplicates;
         sorted_ = false;
     }
     // src/Splats.cpp:346-354
     void sort() {
         if (sorted_) return;  // already sorted this frame (computeBins ran first)
-        report(gs_sort(ctx_.get()), ctx_.get());
+        report(gs_sort(ctx_->get()), ctx_->get());
         sorted_ = true;
     }
     // src/Splats.cpp:481-512.  Tile ranges are taken from the sorted entries, so when the
     // reference's call order (bins before sort) is used the sort is run first.
     void computeBins() {
         if (!sorted_) sort();
-        report(gs_compute_bins(ctx_.get()), ctx_.get());
+        report(gs_compute_bins(ctx_->get()), ctx_->get());
     }
     // src/Splats.cpp:356-381
     void draw(int width, int height, float tileWidth, float tileHeight) {
         ensureTexture(width, height);
-        report(gs_draw(ctx_.get(), scene_, width, height, tileWidth, tileHeight, flags_, texture_, 1), ctx_.get());
+        report(gs_draw(ctx_->get(), scene_, width, height, tileWidth, tileHeight, flags_, texture_, 1), ctx_->get());
     }
     // src/Splats.cpp:383-412 presents the texture; headless: copy it to the host (row 0 = GL row 0)
     std::vector<uint8_t> display() const {
         std::vector<uint8_t> img((size_t)width_ * height_ * 4);
-        report(gs_memcpy_d2h(ctx_.get(), img.data(), texture_, img.size()), ctx_.get());
+        report(gs_memcpy_d2h(ctx_->get(), img.data(), texture_, img.size()), ctx_->get());
         return img;
     }
     void *texture() const { return texture_; }  // device RGBA8
@@ -246,7 +254,16 @@ class Splats {
     std::vector<vec4> rotations;
     std::vector<float> covarianceMatrices;
 
+    Context &context() const { return *ctx_; }
+
   private:
+    void setup(const std::string &filePath, int width, int height) {
+        std::cout << "setting up splats" << std::endl;
+        loadSplats(filePath);
+        computeCovarianceMatrices();
+        loadToGPU(width, height);
+        std::cout << "finished setting up splats" << std::endl;
+    }
     // src/Splats.cpp:174-344
     void loadSplats(const std::string &filePath) {
         std::cout << "Loading splats from file" << std::endl;
@@ -277,14 +294,15 @@ class Splats {
             height_ = height;
             return;
         }
-        if (texture_) gs_free(ctx_.get(), texture_);
+        if (texture_) gs_free(ctx_->get(), texture_);
         texture_ = nullptr;
-        report(gs_malloc(ctx_.get(), (size_t)width * height * 4, &texture_), ctx_.get());
+        report(gs_malloc(ctx_->get(), (size_t)width * height * 4, &texture_), ctx_->get());
         width_ = width;
         height_ = height;
     }
 
-    Context &ctx_;
+    Context *ctx_ = nullptr;
+    std::unique_ptr<Context> own_;  // created when no Context was current
     uint32_t flags_ = 0;
     gs_scene *scene_ = nullptr;
     void *texture_ = nullptr;

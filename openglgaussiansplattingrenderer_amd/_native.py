@@ -116,12 +116,14 @@ SIGNATURES = {
     "gs_ctx_set_draw_sub": (_i, [_vp, _i, ctypes.POINTER(_i)]),
     "gs_ctx_set_small_limits": (_i, [_vp, ctypes.c_int64, ctypes.c_int64]),
     "gs_ctx_set_bucket_sort": (_i, [_vp, _i]),
+    "gs_ctx_set_lookback_spin": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_uint64)]),
     "gs_prefix_stats": (_i, [_vp, _vp, _i]),
     "gs_malloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),
     "gs_free": (_i, [_vp, _vp]),
     "gs_memcpy_h2d": (_i, [_vp, _vp, _vp, _sz]),
     "gs_memcpy_d2h": (_i, [_vp, _vp, _vp, _sz]),
     "gs_memset": (_i, [_vp, _vp, _i, _sz]),
+    "gs_stream_copy_gbs": (_i, [_vp, _sz, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),
     "gs_ply_count": (_i, [ctypes.c_char_p, ctypes.POINTER(_i)]),
     "gs_ply_load": (_i, [ctypes.c_char_p, _i, _vp, _vp, _vp, _vp, _vp]),
     "gs_ply_write": (_i, [ctypes.c_char_p, _i, _vp, _vp, _vp, _vp, _vp]),

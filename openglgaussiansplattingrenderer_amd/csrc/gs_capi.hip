@@ -165,7 +165,11 @@ struct gs_ctx {
     bool bucket_sort = true;
     // [256] per tile: the deepest window position recent blends reached (gs::PrefixDev::depth);
     // allocated with the first prefix-sorted frame, shared by the lanes
-    uint32_t *prefix_depth = nullptr;  // the small sort form: by tile, then per tile (3 launches); else 8 launches
+    uint32_t *prefix_depth = nullptr;
+    // k_pre_emit's bounded look-back wait (gs_ctx_set_lookback_spin) and the fused frames
+    // rendered again because a wait gave up
+    uint32_t lb_spin = gs::kLbSpinLimit;
+    uint64_t lb_redo = 0;
 };
 
 struct gs_scene {
@@ -391,7 +395,11 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
             // a prefix-sorted frame whose blend reached an unsorted position: render it again
             // (full sort) and sort deeper from now on
-            const bool miss = sl.prefix && ctx->h_ring[4 * k + 2] != 0;
+            const uint32_t flag = ctx->h_ring[4 * k + 2];
+            const bool miss = sl.prefix && flag == 1u;
+            // ... or a fused frame (k_pre_emit) whose look-back wait gave up: its entries were
+            // placed from partial offsets (render it again; the depth stays)
+            const bool lb_fail = sl.fused && flag == 2u;
             // ... or that kept more entries than its sort passes could hold (sized from earlier frames)
             const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
             if (sl.prefix) {
@@ -411,7 +419,8 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             if (miss || full) ctx->prefix_redo += 1;
             // the split layout of a fused frame holds its duplicates from index n on
             const int64_t need = sl.fused ? (int64_t)sl.n + D : V + D;
-            if (need > sl.cap || miss || full) return handle_overflow(ctx);
+            if (lb_fail) ctx->lb_redo += 1;
+            if (need > sl.cap || miss || full || lb_fail) return handle_overflow(ctx);
             ctx->V = V;
             ctx->D = D;
             ctx->E = V + D;
@@ -455,6 +464,10 @@ int begin_frame(gs_ctx *ctx) {
         const int k = (ctx->cur + 1) % kRing;
         if (!ctx->slot[k].used) {
             ctx->cur = k;
+            // the frame's flag word (k_draw: a prefix miss = 1; k_pre_emit: a look-back that gave
+            // up = 2) starts clear; the kernels only ever store nonzero flags to it.  (The slot's
+            // previous frame is retired, so nothing on the device writes it now.)
+            ctx->h_ring[4 * k + 2] = 0;
             ctx->slot[k] = gs_ctx::Slot{};
             ctx->slot[k].used = true;
             ctx->slot[k].seq = ++ctx->seq;
@@ -951,7 +964,7 @@ int enqueue_pre_emit(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, u
                         u->view[4 * c + 2] * u->view[14]);
     Lane &L = *ctx->L;
     uint64_t *cur = L.lb + (size_t)L.lb_par * L.lb_cap, *nxt = L.lb + (size_t)(L.lb_par ^ 1) * L.lb_cap;
-    gs::LookbackDev lb{cur, nxt, L.lb_cap};
+    gs::LookbackDev lb{cur, nxt, L.lb_cap, ctx->lb_spin};
     L.lb_par ^= 1;
     gs::launch_pre_emit(L.stream, P, scene_dev(scene), frame_dev(ctx), lb, lazy_loads(ctx, n), L.keys, L.vals, (uint32_t)L.e_cap,
                         prefix_hist, fev(ctx, 0), fev(ctx, 1));
@@ -1339,6 +1352,13 @@ int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
     if (target >= 0) {
         ctx->prefix_base = ctx->prefix_target = target;
         ctx->prefix_clean_run = 0;
+        if (ctx->prefix_depth) {  // a new target starts from a cold per-tile depth table (after the
+            // frames in flight, whose blends write it)
+            if (int rc = use_device(ctx)) return rc;
+            if (int rc = validate_all(ctx)) return rc;
+            if (int rc = sync_lanes(ctx)) return rc;
+            GS_HIP(ctx, hipMemset(ctx->prefix_depth, 0, 256 * 4));
+        }
     }
     if (current) *current = ctx->prefix_target;
     return GS_OK;
@@ -1355,6 +1375,13 @@ int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (on >= 0) ctx->bucket_sort = on != 0;
     return ctx->bucket_sort ? 1 : 0;
+}
+
+int gs_ctx_set_lookback_spin(gs_ctx *ctx, int limit, uint64_t *redone) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (limit >= 0) ctx->lb_spin = (uint32_t)limit;
+    if (redone) *redone = ctx->lb_redo;
+    return (int)std::min<uint32_t>(ctx->lb_spin, 0x7fffffffu);
 }
 
 int gs_ctx_set_draw_sub(gs_ctx *ctx, int sub, int *current) {

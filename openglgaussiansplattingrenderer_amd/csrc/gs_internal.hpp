@@ -246,7 +246,12 @@ struct LookbackDev {
     uint64_t *st;          // [cap_blocks] this frame's per-workgroup status words (zero on entry)
     uint64_t *st_next;     // the other half, cleared by this frame
     uint32_t cap_blocks;
+    // polls a workgroup spends waiting on a predecessor before it gives up, emits at the offsets
+    // it has and flags the frame (ring word 2 = 2) for the host to render again; 0 gives up at
+    // once (gs_ctx_set_lookback_spin: the test that drives the re-render)
+    uint32_t spin_limit;
 };
+constexpr uint32_t kLbSpinLimit = 1u << 15;
 // mains at [0, V), duplicates at [n, n + D) of keys / vals (the sort's first pass reads them as
 // one array, sort_pairs' dup_base); (V, D) into fr.totals and the frame's pinned ring slot.
 // lazy: the covariance / opacity loads only for the splats inside the NDC square.

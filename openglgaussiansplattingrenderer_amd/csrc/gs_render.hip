@@ -628,7 +628,6 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, in
         if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
             fr.h_totals[0] = s_carry[0];
             fr.h_totals[1] = s_carry[1];
-            fr.h_totals[2] = 0;  // the prefix-sort miss flag (k_draw)
             fr.h_totals[3] = 0;
         }
     }
@@ -828,7 +827,6 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
 // instead of the workgroup id serialised every workgroup's start on one address: ~33 ns each,
 // 0.2 ms for the 6000 workgroups of C3.)
 constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62;
-constexpr uint32_t kLbSpinLimit = 1u << 15;
 __device__ __forceinline__ uint64_t lb_word(uint64_t flag, uint32_t m, uint32_t d) {
     return flag | ((uint64_t)(d & 0x7fffffffu) << 31) | (uint64_t)(m & 0x7fffffffu);
 }
@@ -897,7 +895,8 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
             if (lane == 0) lb_store(&lb.st[0], lb_word(kLbInc, all_m, all_d));
         } else {
             if (lane == 0) lb_store(&lb.st[blk], lb_word(kLbAgg, all_m, all_d));
-            int j = (int)blk - 1;  // the window's nearest predecessor
+            fail = lb.spin_limit == 0;  // (test hook: give up at once)
+            int j = fail ? -1 : (int)blk - 1;  // the window's nearest predecessor
             uint32_t spins = 0;
             while (j >= 0) {  // uniform
                 const int idx = j - lane;
@@ -908,7 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
                 const int fp = inc ? __builtin_ctzll(inc) : 63;  // lanes 0..fp are needed
                 const uint64_t need = fp == 63 ? ~0ull : ((2ull << fp) - 1ull);
                 if (notready & need) {
-                    if (++spins > kLbSpinLimit) {
+                    if (++spins > lb.spin_limit) {
                         fail = true;
                         break;
                     }
@@ -924,7 +923,10 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
         }
         if (lane == 0) {
             s_off = make_uint2(exm, exd);
-            if (fail && fr.h_totals) fr.h_totals[2] = 2u;  // (never expected) the frame is rendered again
+            // (never expected) the frame is rendered again.  Word 2 is cleared by the host when the
+            // slot is taken, and nothing on the device writes 0 to it during the frame: a plain
+            // store of a nonzero flag (k_draw's prefix miss writes 1) cannot be lost
+            if (fail && fr.h_totals) fr.h_totals[2] = 2u;
             if (blk == nblocks - 1) {  // the last workgroup: the frame's (V, D)
                 // the device count holds the duplicates emitted (below cap: a frame that did not fit
                 // is detected by the host from the pinned count, and rendered again), so every
@@ -934,7 +936,6 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
                 if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
                     fr.h_totals[0] = exm + all_m;
                     fr.h_totals[1] = exd + all_d;
-                    if (!fail) fr.h_totals[2] = 0;  // the prefix-sort miss flag (k_draw)
                     fr.h_totals[3] = 0;
                 }
             }

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ cnt, int shift,
                                                     uint32_t *__restrict__ hist, uint32_t nb,
                                                     uint32_t *__restrict__ tile_counts, PrefixDev pre,
-                                                    uint32_t dup_base, uint32_t *__restrict__ zero_cols) {
+                                                    uint32_t dup_base) {
     constexpr int kThreads = W * 64, kTile = kThreads * IT;
     static_assert(kThreads >= kRadix, "one thread per digit flushes the counts");
     const uint32_t n = elem_count(n_max, cnt);
@@ -272,10 +272,6 @@ __global__ __launch_bounds__(W * 64) void k_upsweep(const uint32_t *__restrict__
     const int d = threadIdx.x;
     if (d >= kRadix) return;
     hist[(size_t)d * nb + tile] = sum8(&s_cnt[d * kRep]);
-    if (zero_cols) {  // the small sort: this tile's columns of passes 1-3 (k_sweep_small adds into them)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) zero_cols[((size_t)q * kRadix + d) * nb + tile] = 0u;
-    }
     if (TILES) {
         const uint32_t c = sum8(&s_tiles[d * kRep]);
         if (c) atomicAdd(&tile_counts[(blockIdx.x % kTileCopies) * kRadix + d], c);
@@ -1105,7 +1101,17 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     // the class's target: the configured one, or less where recent blends read the list
     // shallowly (the depth word was read before the scan's barriers; its decay written after)
     const uint32_t target = dep ? min(pre.target, 2u * dep + kPrefixDepthSlack) : pre.target;
-    if (pre.depth && j == 0) pre.depth[c] = dep - (dep >> 4);
+    // (decayed by a CAS loop on the current word, not a store of dep - dep / 16: with frames in
+    // flight another lane's blend may have raised it since it was read, and a plain store would
+    // drop that maximum)
+    if (pre.depth && j == 0 && dep) {
+        uint32_t cur = dep;
+        for (int tries = 0; tries < 16; ++tries) {
+            const uint32_t seen = atomicCAS(&pre.depth[c], cur, cur - (cur >> 4));
+            if (seen == cur) break;
+            cur = seen;
+        }
+    }
     const uint32_t tgt = (target + kPrefixSample - 1) / kPrefixSample;
     const uint32_t hi = class_hi(c);
     if (c == 0 && j == 0) pre.theta[256] = 0xffffffffu;  // class 256 is kept whole
@@ -1244,8 +1250,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
                           : (bk ? (t1k ? k_upsweep<kWaveSmall, false, false, true, kItems / 4> : k_upsweep<kWaveSmall, false, false, true>)
                                 : k_upsweep<kWaveSmall, false>);
             hipExtLaunchKernelGGL(up, dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr, 0, kin, (uint32_t)n,
-                                  dev_count, 8 * pass, sc.hist, nb, pass == 0 && bins ? tile_counts : nullptr, PrefixDev{}, sp,
-                                  nullptr);
+                                  dev_count, 8 * pass, sc.hist, nb, pass == 0 && bins ? tile_counts : nullptr, PrefixDev{}, sp);
             const dim3 grid(nb + ((pass == 0 && bins && !bk) ? 1 : 0));
             auto sw = bk ? (t1k ? k_sweep_small<true, kItems / 4> : k_sweep_small<true>) : k_sweep_small<false>;
             hipExtLaunchKernelGGL(sw, grid, dim3(kWaveSmall * 64), 0, s, nullptr, bk ? nullptr : e1, 0, kin, vin, kout, vout,
@@ -1295,19 +1300,19 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const uint32_t split = (pass == 0 && dup_base >= 0) ? (uint32_t)dup_base : kNoSplit;
         if (big && pre)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split, nullptr);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
         else if (big && bins)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split, nullptr);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
         else if (big && all_big && GS_UPSWEEP_REV)  // (standalone sorts of >= 16M keys)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false, false, false, kItems, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64),
-                                  0, s, e0, nullptr, 0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split, nullptr);
+                                  0, s, e0, nullptr, 0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split);
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
-                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split, nullptr);
+                                  kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split);
         else
             hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
-                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, kNoSplit, nullptr);
+                                  0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, kNoSplit);
         // one more workgroup scans the tile counts in the last pass (a prefix sort: with the draw
         // limits; and one in the first pass makes the class tables passes 1-3 need)
         const bool with_bins = bins && (pass == 3 || (pre && pass == 0));

@@ -73,6 +73,15 @@ class Context:
         check(min(r, 0), self.handle)
         return r
 
+    def set_lookback_spin(self, limit: int = -1):
+        """gs_ctx_set_lookback_spin: polls the fused preprocess + emission's look-back waits before
+        it gives up and the frame is rendered again (0: at once, a test hook; -1 leaves it).
+        Returns (limit, frames rendered again for it)."""
+        red = ctypes.c_uint64()
+        r = lib().gs_ctx_set_lookback_spin(self.handle, int(limit), ctypes.byref(red))
+        check(min(r, 0), self.handle)
+        return r, int(red.value)
+
     def set_draw_sub(self, sub: int = -1) -> int:
         """the blend's sub-block form (gs_ctx_set_draw_sub): 0 by entry count (default), 8 (one
         pixel per lane, small frames) or 16 (2x2 quads per lane, large frames); -1 leaves it.

@@ -81,11 +81,14 @@ int main(int argc, char **argv) {
     if (!ctx.get()) return 3;
     if (sort_test(ctx)) return 1;
     {
-        gs::Splats splats(argv[1], 100, 100, ctx);  // plyParseTests.cpp:105-109
+        // plyParseTests.cpp:105-109 and main.cpp:47: the reference's three arguments (the scene
+        // goes to the current Context, as the reference's buffers go to the current GL context)
+        gs::Splats splats(argv[1], 100, 100);
         EXPECT(splats.numSplats == 1);
+        EXPECT(&splats.context() == &ctx);
     }
     {
-        gs::Splats splats(argv[1], 256, 256, ctx);
+        gs::Splats splats(argv[1], 256, 256);
         const gs_uniforms u = gs::main_pose_uniforms(256, 256);
         gs::mat4 view, vp;
         std::memcpy(view.m, u.view, sizeof(view.m));
@@ -102,6 +105,12 @@ int main(int argc, char **argv) {
         std::thread([other] { delete other; }).join();
         EXPECT(gs::Context::current() == nullptr);
         EXPECT(gs::GPURadixSort(1u, 3u, 2u, nullptr, nullptr, nullptr, 0, 16, 32, nullptr) == GS_ERR_STATE);
+        {  // no Context current: the three-argument Splats creates (and makes current) its own
+            gs::Splats own(argv[1], 64, 64);
+            EXPECT(own.numSplats == 1);
+            EXPECT(gs::Context::current() == &own.context() && &own.context() != &ctx);
+        }
+        EXPECT(gs::Context::current() == nullptr);
         ctx.makeCurrent();
         EXPECT(gs::Context::current() == &ctx);
     }

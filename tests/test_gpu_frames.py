@@ -85,6 +85,40 @@ def test_overflow_renders_again():
     ctx.close()
 
 
+def test_lookback_giveup_renders_again():
+    """the fused preprocess + emission (k_pre_emit, scenes of <= 64k splats) bounds each
+    look-back wait; a workgroup that gives up emits at partial offsets and flags the frame (ring
+    word 2 = 2), which the host renders again on the synchronous path.  Spin limit 0 makes every
+    workgroup after the first give up at once: every frame in flight is redone, and the images
+    still equal the synchronous frames; with the limit back, none is"""
+    W, H = 512, 384
+    ctx = g.Context(0)
+    means, rot, sc, op, col = c2_scene()
+    sp = g.Splats.from_raw(means, col, np.log(op / (1 - op)), np.log(sc), rot, W, H, ctx=ctx)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(5)]
+    render_sync(sp, pose(W, H, 0), outs[0])  # counts seen once
+    limit, red0 = ctx.set_lookback_spin(0)
+    assert limit == 0
+    for k in range(5):
+        render_spec(sp, pose(W, H, k), outs[k])
+    ctx.sync()
+    got = [o.download(np.uint8, W * H * 4) for o in outs]
+    _, red1 = ctx.set_lookback_spin(1 << 15)
+    assert red1 - red0 >= 1, "the give-up path must have run"
+    for k in range(5):
+        render_spec(sp, pose(W, H, k), outs[k])
+    ctx.sync()
+    again = [o.download(np.uint8, W * H * 4) for o in outs]
+    assert ctx.set_lookback_spin(-1)[1] == red1, "no frame redone with the default limit"
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    for k in range(5):
+        render_sync(sp, pose(W, H, k), ref)
+        r = ref.download(np.uint8, W * H * 4)
+        assert np.array_equal(got[k], r), f"pose {k} (given up)"
+        assert np.array_equal(again[k], r), f"pose {k}"
+    ctx.close()
+
+
 def test_staged_calls_after_inflight_frames():
     """the stage API validates frames in flight first (counts on the host, results intact)"""
     W, H = 256, 256

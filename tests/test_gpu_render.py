@@ -4,6 +4,7 @@ the committed golden fixtures.
 Bar: means2D, conics, keys, sorted entries and bins bit-exact; RGBA8 bit-exact
 with the defined exp (default), and >= 99.9% of covered pixels within +-1 LSB, max +-2 LSB
 with GS_FLAG_FAST_EXP (hardware v_exp_f32)."""
+import ctypes
 import os
 import tempfile
 
@@ -11,6 +12,7 @@ import numpy as np
 import pytest
 
 import openglgaussiansplattingrenderer_amd as g
+from openglgaussiansplattingrenderer_amd import _native as N
 from tests.golden.make_golden import U
 
 pytestmark = pytest.mark.gpu
@@ -134,6 +136,112 @@ def test_queued_preprocess_on_mostly_culled_frames(oracle, W, H, turn, flags):
         for k in ("means2d", "conics", "keys", "vals", "bins"):
             assert_bits(r[k], o[k], f"{frame}/{k}")
         assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{frame}/image")
+
+
+def depth_range_scene(u, n=20_000, seed=5, log_scale=-7.0, opacity_bias=0.0):
+    """n tiny splats at random NDC x, y in [-0.95, 0.95] and NDC depth in [-1.5, 2.5]: in ref mode
+    there is no near/far cull (preprocess.glsl:77-89), so the keys tile + z01 (:154) run outside
+    [tile, tile + 1) -- below their tile, negative floats (which sort last as words but bin to
+    tile 0, countBins.glsl:25-29) and past tile + 1 into the next tiles' ranges"""
+    rng = np.random.default_rng(seed)
+    VP = np.array(u.vp[:], np.float64).reshape(4, 4).T
+    ndc = np.stack([rng.uniform(-0.95, 0.95, n), rng.uniform(-0.95, 0.95, n), rng.uniform(-1.5, 2.5, n),
+                    np.ones(n)], 1)
+    w = (np.linalg.inv(VP) @ ndc.T).T
+    means = (w[:, :3] / w[:, 3:]).astype(np.float32)
+    col = rng.normal(0, 0.8, (n, 3)).astype(np.float32)
+    op = (rng.normal(0, 2, n) + opacity_bias).astype(np.float32)
+    return means, col, op, np.full((n, 3), log_scale, np.float32), rng.normal(size=(n, 4)).astype(np.float32)
+
+
+# the frame sort's forms: (bucket sort, small-sort entry limit, prefix target)
+SORT_FORMS = {
+    "bucket": (1, 512 << 10, 0),      # by tile, then each tile's list (3 launches)
+    "four_pass": (0, 512 << 10, 0),   # k_sweep_small: four 8-bit passes (8 launches)
+    "full": (0, 0, 0),                # upsweep / row scan / downsweep per pass (12 launches)
+    "prefix_whole": (0, 0, None),     # prefix sort, classes below the target kept whole
+    "prefix_cut": (0, 0, 1024),       # prefix sort, lists cut (an opaque scene: blends saturate)
+    "prefix_partial": (0, 0, 64),     # prefix sort of 64-entry prefixes (misses re-rendered)
+}
+
+
+@pytest.mark.parametrize("form", list(SORT_FORMS))
+@pytest.mark.parametrize("W,H,n", [(512, 512, 80_000), (1920, 1080, 80_000)])
+def test_out_of_range_keys_every_sort_form(oracle, form, W, H, n):
+    """ref-mode keys outside their tile's [t, t+1) (depth_range_scene: negative, below the tile,
+    past t + 1) through every form of the frame sort, at 512x512 and 1080p: keys, values, bins
+    and image of three consecutive frames (the first host-synchronous, the others enqueued without
+    a round trip) bit-exact against the oracle.  The prefix forms run on frames of >= 64 x target
+    entries; with the whole classes kept no frame may be rendered again."""
+    bucket, small_sort, target = SORT_FORMS[form]
+    ctx = g.Context(0)
+    u = g.main_camera(W, H).uniforms()
+    if form == "prefix_cut":  # larger, mostly opaque splats: the blends saturate within the prefix
+        mm, cc, oo, ls, rr = depth_range_scene(u, n, log_scale=-4.5, opacity_bias=4.0)
+    else:
+        mm, cc, oo, ls, rr = depth_range_scene(u, n)
+    sp = g.Splats.from_raw(mm, cc, oo, ls, rr, W, H, ctx=ctx)
+    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0)
+    if target is None:  # the deepest target the frame allows (E >= 64 x target): ~4x the mean
+        target = o["E"] // 64  # class, so the sampled classes stay below it and are kept whole
+    assert ctx.set_bucket_sort(bucket) == bucket
+    ctx.set_small_limits(-1, small_sort)
+    ctx.set_sort_prefix(target)
+    keys = o["keys"].view(np.float32)
+    assert (keys < 0).any(), "negative keys expected (splats in front of the near plane)"
+    assert o["E"] >= 64 * max(target, 1)
+    ctx.prefix_stats(reset=True)
+    for frame in range(3):
+        r = gpu_frame(sp, u, 0)
+        assert [r["V"], r["D"], r["E"]] == [o["V"], o["D"], o["E"]], frame
+        for k in ("keys", "vals", "bins"):
+            assert_bits(r[k], o[k], f"{form} frame {frame}/{k}")
+        assert_bits(r["image"].reshape(-1), o["image"].reshape(-1), f"{form} frame {frame}/image")
+    ps = ctx.prefix_stats()
+    print(form, W, H, "E", o["E"], "target", target, ps)
+    if form.startswith("prefix"):
+        assert ps["frames"] >= 2, ps
+        if form == "prefix_whole":  # the prefix machinery sorted every entry, nothing redone
+            assert ps["redone"] == 0 and ps["kept"] == o["E"], ps
+        if form == "prefix_cut":  # lists cut and the cut lists' images still exact, nothing redone
+            assert ps["redone"] == 0 and ps["kept"] < o["E"], ps
+    else:
+        assert ps["frames"] == 0, ps
+    ctx.close()
+
+
+@pytest.mark.parametrize("bucket", [1, 0])
+def test_zero_entry_frames_then_bucket_sort(oracle, bucket):
+    """a context's first frame has no entries (every splat off screen), then frames of
+    out-of-range keys follow, alternating with empty ones, on rotating outputs: the small sort's
+    tables after a sort of zero keys hold nothing stale -- every image equals the oracle's"""
+    W, H = 512, 512
+    ctx = g.Context(0)
+    assert ctx.set_bucket_sort(bucket) == bucket
+    u = g.main_camera(W, H).uniforms()
+    mm, cc, oo, ls, rr = depth_range_scene(u, 20_000, seed=11)
+    full = g.Splats.from_raw(mm, cc, oo, ls, rr, W, H, ctx=ctx)
+    far = mm.copy()
+    far[:, 0] += 1.0e5  # off screen: no entries
+    empty = g.Splats.from_raw(far, cc, oo, ls, rr, W, H, ctx=ctx)
+    of = oracle.render(full.means3D, full.covarianceMatrices, full.opacities, full.colours, u, flags=0)
+    oe = oracle.render(empty.means3D, empty.covarianceMatrices, empty.opacities, empty.colours, u, flags=0)
+    assert oe["E"] == 0 and of["E"] > 0
+    seq = [empty, empty, full, empty, full, full, empty]
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in seq]
+    check_first = gpu_frame(empty, u, 0)  # host-synchronous (the context's first frame)
+    assert check_first["E"] == 0 and np.array_equal(check_first["image"], oe["image"])
+    for sp, out in zip(seq, outs):  # enqueued without a round trip
+        N.check(N.lib().gs_render(ctx.handle, sp._scene, ctypes.byref(u), 0, out.ptr, 1, None), ctx.handle)
+    ctx.sync()
+    for k, (sp, out) in enumerate(zip(seq, outs)):
+        ref = of if sp is full else oe
+        got = out.download(np.uint8, W * H * 4)
+        assert_bits(got, ref["image"].reshape(-1), f"frame {k} ({'full' if sp is full else 'empty'})")
+    r = gpu_frame(full, u, 0)
+    for k in ("keys", "vals", "bins"):
+        assert_bits(r[k], of[k], f"after the sequence/{k}")
+    ctx.close()
 
 
 @pytest.mark.parametrize("bucket", [1, 0])
