@@ -904,13 +904,22 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 
 // covariance loads only for the splats inside the NDC square when the newest frame seen had most
 // of the scene's splats culled (the small C5 views)
+// GS_FLAG_SH frames prefix-sorted: SH colours for the kept entries' splats only (k_sh_kept)
+#ifndef GS_SH_KEPT
+#define GS_SH_KEPT 1
+#endif
+constexpr bool kShKept = GS_SH_KEPT != 0;
+
 #ifndef GS_QUEUE_FRAC
 #define GS_QUEUE_FRAC 2  // the queued preprocess when fewer than n / GS_QUEUE_FRAC splats were visible
 #endif
 bool lazy_loads(const gs_ctx *ctx, int n) { return ctx->n == n && ctx->e_known && ctx->V * GS_QUEUE_FRAC < (int64_t)n; }
 
-// preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->L->totals
-int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags) {
+// preprocess + block-sum scan of a new frame (events 0, 1); (V, D) land in ctx->L->totals.
+// defer_sh (a prefix-sorted GS_FLAG_SH frame): no SH colours here -- k_sh_kept colours the kept
+// entries' splats after the sort (enqueue_sh_kept)
+int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
+                       bool defer_sh = false) {
     const int n = scene->n;
     const bool sh = (flags & GS_FLAG_SH) != 0;
     if (sh && !scene->sh) return set_error(ctx, GS_ERR_INVALID, "GS_FLAG_SH: the scene has no SH (gs_scene_set_sh)");
@@ -931,7 +940,9 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     const gs::FrameDev fr = frame_dev(ctx);
     const int nb = gs::preprocess_blocks(n);
     // k_scan_blocksums writes (V, D) to ctx->L->totals and to this slot's pinned host copy
-    gs::launch_preprocess(ctx->L->stream, P, scene_dev(scene), fr, fev(ctx, 0), lazy_loads(ctx, n));
+    gs::PreParams Pl = P;
+    if (defer_sh) Pl.sh = 0;
+    gs::launch_preprocess(ctx->L->stream, Pl, scene_dev(scene), fr, fev(ctx, 0), lazy_loads(ctx, n));
     gs::launch_scan_blocksums(ctx->L->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
@@ -1157,10 +1168,12 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
     }
     const bool fused = gs::preprocess_blocks(scene->n) <= kFusedMaxBlocks;
+    // GS_FLAG_SH with the prefix sort: colour only the kept entries' splats, after the sort
+    const bool defer_sh = prefix && !fused && (flags & GS_FLAG_SH) && kShKept;
     if (fused) {
         if (int rc = enqueue_pre_emit(ctx, scene, u, flags, prefix ? pd.hist : nullptr)) return rc;
     } else {
-        if (int rc = enqueue_preprocess(ctx, scene, u, flags)) return rc;
+        if (int rc = enqueue_preprocess(ctx, scene, u, flags, defer_sh)) return rc;
     }
     gs_ctx::Slot &sl = ctx->slot[ctx->cur];
     sl.spec = true;
@@ -1186,6 +1199,11 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
                            ctx->E < ctx->small_sort_entries)))
         return rc;
+    if (defer_sh) {  // the kept entries' values: the sort's pass-2 output, left in the alternate buffer
+        gs::launch_sh_kept(ctx->L->stream, ctx->L->pe_P, scene_dev(scene), frame_dev(ctx), ctx->L->sort.vals_alt,
+                           pd.nsel, pd.cap_sel);
+        GS_HIP(ctx, hipGetLastError());
+    }
     if ((rc = enqueue_draw(ctx, scene, u->width, u->height, (float)u->width / 16.f, (float)u->height / 16.f, flags,
                            out, 1, ctx->L->e_cap, cnt, prefix)))
         return rc;

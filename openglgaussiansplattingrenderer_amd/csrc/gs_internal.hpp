@@ -235,6 +235,10 @@ int pre_emit_blocks(int n);    // workgroups of k_pre_emit (= its look-back stat
 void launch_preprocess(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
                        bool lazy = false);
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop);
+// GS_FLAG_SH colours of a prefix-sorted frame after its sort (P.sh was cleared for its preprocess):
+// the splats of ids[0, min(count[0], cap)) -- the kept entries -- and splat 0
+void launch_sh_kept(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const uint32_t *ids,
+                    const uint32_t *count, uint32_t cap);
 bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preprocess) fits this frame
 // prefix_hist != null: also sample the emitted keys into the prefix sort's histogram
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,

@@ -160,7 +160,7 @@ SORT_FORMS = {
     "four_pass": (0, 512 << 10, 0),   # k_sweep_small: four 8-bit passes (8 launches)
     "full": (0, 0, 0),                # upsweep / row scan / downsweep per pass (12 launches)
     "prefix_whole": (0, 0, None),     # prefix sort, classes below the target kept whole
-    "prefix_cut": (0, 0, 1024),       # prefix sort, lists cut (an opaque scene: blends saturate)
+    "prefix_cut": (0, 0, 4096),       # prefix sort, lists cut (larger, mostly opaque splats)
     "prefix_partial": (0, 0, 64),     # prefix sort of 64-entry prefixes (misses re-rendered)
 }
 
@@ -203,8 +203,10 @@ def test_out_of_range_keys_every_sort_form(oracle, form, W, H, n):
         assert ps["frames"] >= 2, ps
         if form == "prefix_whole":  # the prefix machinery sorted every entry, nothing redone
             assert ps["redone"] == 0 and ps["kept"] == o["E"], ps
-        if form == "prefix_cut":  # lists cut and the cut lists' images still exact, nothing redone
+        if form == "prefix_cut" and W == 512:  # lists cut, and the cut lists gave the exact images
             assert ps["redone"] == 0 and ps["kept"] < o["E"], ps
+        # (at 1080p these splats are too small for any block to saturate: every cut frame misses
+        # and is rendered again on the synchronous path -- the images above are still exact)
     else:
         assert ps["frames"] == 0, ps
     ctx.close()

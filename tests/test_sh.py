@@ -104,3 +104,44 @@ def test_sh_flag_needs_sh(tmp_path):
     with pytest.raises(g.GsError, match="no SH"):
         sp.render_uniforms(g.main_camera(64, 64).uniforms())
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("target", ["whole", 512])
+def test_sh_prefix_sorted_frames_colour_kept_splats(tmp_path, target):
+    """a prefix-sorted GS_FLAG_SH frame colours only its kept entries' splats, after the sort
+    (k_sh_kept): frames enqueued without a round trip, over two poses, bit-exact against the
+    oracle's SH colours -- with every class kept whole (no frame may be redone, so the kept-splat
+    colours made the images) and with cut lists (misses re-rendered on the synchronous path)"""
+    from oracle import oracle as O
+    O.build()
+    W, H = 1280, 720
+    ctx = g.Context(0)
+    means, f_dc, f_rest, logit, log_scale, rot = sh_scene(100_000, seed=11)  # > 64k: not the fused kernel
+    p = str(tmp_path / "sh_big.ply")
+    write_ply_with_sh(p, means, f_dc, f_rest, logit, log_scale, rot)
+    sp = g.Splats(p, W, H, ctx=ctx, sh=True)
+    sp.flags = g.GS_FLAG_SH
+    poses = []
+    for turn in (0.0, 4.0):
+        cam = g.main_camera(W, H)
+        cam.rotateRight(turn)
+        poses.append(cam.uniforms())
+    refs = []
+    for u in poses:
+        cols = O.sh_colours(sp.means3D, f_dc, f_rest, np.array(u.view, np.float32), np.ones(sp.numSplats, np.uint8),
+                            sp.colours)
+        refs.append(O.render(sp.means3D, sp.covarianceMatrices, sp.opacities, cols, u, flags=0, stages=False))
+    E = min(r["E"] for r in refs)
+    ctx.set_sort_prefix(E // 64 if target == "whole" else target)
+    sp.render_uniforms(poses[0])  # host-synchronous (the context's first frame)
+    assert np.array_equal(sp.texture().reshape(-1), refs[0]["image"].reshape(-1))
+    ctx.prefix_stats(reset=True)
+    for k in range(4):
+        sp.render_uniforms(poses[k % 2])
+        assert np.array_equal(sp.texture().reshape(-1), refs[k % 2]["image"].reshape(-1)), f"frame {k}"
+    ps = ctx.prefix_stats()
+    assert ps["frames"] >= 1, ps
+    if target == "whole":
+        assert ps["redone"] == 0, ps
+    ctx.close()
