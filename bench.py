@@ -272,9 +272,11 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
             poses.append(cam.uniforms())
         row = {"deg_per_frame": d, "frames": steps, "pan_deg": round(d * (steps - 1), 2)}
         for mode, tgt in (("prefix", base), ("full_sort", 0)):
-            ctx.set_sort_prefix(tgt)  # (clears the per-tile depths: a cold start)
+            ctx.set_sort_prefix(0)
             ctx.set_lanes(1)
+            sp.render_uniforms(poses[0])  # buffers sized for the first pose (the last run ended elsewhere)
             ctx.sync()
+            ctx.set_sort_prefix(tgt)  # (clears the per-tile depths: a cold start)
             t0 = time.perf_counter()
             sp.render_uniforms(poses[0])
             ctx.sync()
@@ -302,15 +304,15 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
 
 
 def copy_peak(ctx, nbytes: int = 1 << 30, reps: int = 10):
-    """stream-copy rate of this GPU in this run (gs_stream_copy_gbs: float4 grid-stride copy of
-    1 GiB, read + write bytes): the practical HBM ceiling beside the 8 TB/s spec"""
+    """stream-copy rate of this GPU in this run (gs_stream_copy_gbs: non-temporal float4 copy of
+    1 GiB, one per lane, read + write bytes): the practical HBM ceiling beside the 8 TB/s spec"""
     import ctypes
     from openglgaussiansplattingrenderer_amd import _native as native
     med, best = ctypes.c_double(), ctypes.c_double()
     native.check(native.lib().gs_stream_copy_gbs(ctx.handle, nbytes, reps, ctypes.byref(med), ctypes.byref(best)),
                  ctx.handle)
     return dict(gbs_median=round(med.value, 1), gbs_best=round(best.value, 1), bytes=nbytes, reps=reps,
-                source="gs_stream_copy_gbs: float4 grid-stride copy between two 1 GiB buffers, hipEvents, "
+                source="gs_stream_copy_gbs: non-temporal float4 copy (one per lane) between two 1 GiB buffers, hipEvents, "
                        "(read + write bytes) / time, median of %d" % reps)
 
 

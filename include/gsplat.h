@@ -145,7 +145,7 @@ int gs_memcpy_d2h(gs_ctx *ctx, void *dst, const void *src, size_t bytes);
 int gs_memset(gs_ctx *ctx, void *dst, int value, size_t bytes);
 
 /* measurement helper (bench.py's roofline.frac_of_copy; not on the frame path): the stream-copy
- * rate of the ctx's GPU -- a float4 grid-stride copy of `bytes` between two fresh device buffers,
+ * rate of the ctx's GPU -- a non-temporal float4 copy (one per lane) of `bytes` between two fresh device buffers,
  * read + written bytes per second, median (and best) of `reps` hipEvent-timed copies */
 int gs_stream_copy_gbs(gs_ctx *ctx, size_t bytes, int reps, double *gbs_median, double *gbs_best);
 

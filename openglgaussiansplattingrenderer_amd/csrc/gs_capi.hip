@@ -153,6 +153,9 @@ struct gs_ctx {
     int prefix_base = 32768;
     int prefix_target = 32768;
     int prefix_clean_run = 0;
+    // a prefix miss was seen: the next prefix-sorted frame sizes its passes 1-3 for every entry (the
+    // tiles that missed now keep whole windows, so the kept count can jump past the last one)
+    bool prefix_after_miss = false;
     uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
     int prefix_kept_target = 0;  // the depth the frame of prefix_kept was sorted to
     // the blend's sub-block form (gs_ctx_set_draw_sub): 0 by the frame's entry count, 8 or 16
@@ -410,6 +413,7 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             if (miss) {
                 ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
                 ctx->prefix_clean_run = 0;
+                ctx->prefix_after_miss = true;
             } else if (++ctx->prefix_clean_run >= kPrefixDecay) {  // (prefix-sorted or not: a depth that
                 // turned the prefix sort off, E < 64 * target, comes down again too)
                 ctx->prefix_clean_run = 0;
@@ -417,6 +421,7 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
                     ctx->prefix_target = std::max(ctx->prefix_base, ctx->prefix_target / 2);
             }
             if (miss || full) ctx->prefix_redo += 1;
+            if (sl.prefix && !miss && !full && sl.cap_sel >= (uint32_t)sl.cap) ctx->prefix_after_miss = false;
             // the split layout of a fused frame holds its duplicates from index n on
             const int64_t need = sl.fused ? (int64_t)sl.n + D : V + D;
             if (lb_fail) ctx->lb_redo += 1;
@@ -1136,7 +1141,9 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     if (ctx->L->e_cap < want)
         if (int rc = ensure_entries(ctx, want)) return rc;
     // prefix sort: frames of the size where the lists are long (the last observed count)
-    const bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_target;
+    // (enabled by the configured depth, not the doubled one: the per-tile depths keep what each
+    // list needs, and a moving camera's occasional misses must not turn the prefix sort off)
+    const bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_base;
     gs::PrefixDev pd{};
     if (prefix) {
         if (!ctx->L->pre_buf) {
@@ -1157,7 +1164,8 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
                                  ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
                                  : (int64_t)ctx->prefix_kept;
-        pd.cap_sel = (uint32_t)(ctx->prefix_kept ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536) : cap_e);
+        pd.cap_sel = (uint32_t)(ctx->prefix_kept && !ctx->prefix_after_miss ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
+                                                                              : cap_e);
         pd.target = (uint32_t)ctx->prefix_target;
         if (!ctx->prefix_depth) {  // (zeroed before any frame can read it)
             GS_HIP(ctx, hipMalloc(&ctx->prefix_depth, 256 * 4));

@@ -77,6 +77,9 @@ __device__ __forceinline__ M3 tr3(const M3 &a) {
 // operation is IEEE-exact, so CPU == GPU bit for bit.  This is that function on the powers a
 // blend event can carry (x <= 0 or NaN, see needs() in k_draw), where it is the same bits
 // with the underflow branch as a select and the clamp inapplicable.
+// UNDER false: for x known to lie in [-80, 0] (a blend batch whose events cannot reach the
+// underflow cut, k_draw's evsafe): the same bits without the select
+template <bool UNDER = true>
 __device__ __forceinline__ float exp_defined_event(float x) {
     const float kf = rintf(x * 1.44269504088896341f);
     float r = __builtin_fmaf(-kf, 0.693359375f, x);
@@ -90,7 +93,7 @@ __device__ __forceinline__ float exp_defined_event(float x) {
     // p * 2^k: for x in [-80, 0] k is in [-116, 0] and p in [0.7, 1.42], so 2^k and the product
     // are normal and exact: v_ldexp_f32 gives the oracle's p * u2f((k + 127) << 23) in one op
     const float v = __builtin_amdgcn_ldexpf(p, (int)kf);
-    return (x >= -80.0f) ? v : 0.0f;
+    return (UNDER && !(x >= -80.0f)) ? 0.0f : v;
 }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -1234,6 +1237,11 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_DRAW_POWPIX
 #define GS_DRAW_POWPIX 1
 #endif
+// blend batches whose events all have powers in [-80, 0] (GS_EV_SAFE) skip the exp's underflow
+// select: the same bits (see blend_batch)
+#ifndef GS_EV_SAFE
+#define GS_EV_SAFE 1
+#endif
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
@@ -1637,19 +1645,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 const uint32_t pix = s_epix[e];
                 const float power = s_epow[GS_DRAW_POWPIX ? pix : e];
                 float4 col = s_col[pix];
-                const float ex = FAST_EXP ? __expf(power) : exp_defined_event(power);
-                const float alpha = fminf(0.99f, ex * o);
-                const bool take = !(alpha < 1.0f / 255.0f);
-                // alphaBlend :59-67
-                const float remaining = 1.0f - col.w;
-                const float aT = alpha * remaining;
                 if (cfin) {  // uniform: finite colours -- adding rgb * 0 leaves the state as it is
+                    // (and, GS_EV_SAFE, every event's power in [-80, 0]: no underflow select)
+                    const float ex = FAST_EXP ? __expf(power) : exp_defined_event<!GS_EV_SAFE>(power);
+                    const float alpha = fminf(0.99f, ex * o);
+                    const bool take = !(alpha < 1.0f / 255.0f);
+                    // alphaBlend :59-67
+                    const float remaining = 1.0f - col.w;
+                    const float aT = alpha * remaining;
                     const float aZ = take ? aT : 0.0f;
                     col.x = col.x + r * aZ;
                     col.y = col.y + g * aZ;
                     col.z = col.z + bl * aZ;
                     col.w = col.w + aZ;
                 } else {
+                    const float ex = FAST_EXP ? __expf(power) : exp_defined_event(power);
+                    const float alpha = fminf(0.99f, ex * o);
+                    const bool take = !(alpha < 1.0f / 255.0f);
+                    const float remaining = 1.0f - col.w;
+                    const float aT = alpha * remaining;
                     col.x = take ? col.x + r * aT : col.x;
                     col.y = take ? col.y + g * aT : col.y;
                     col.z = take ? col.z + bl * aT : col.z;
@@ -1701,18 +1715,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             if (nb) {  // uniform (no continue: one loop exit)
                 const float o = rl(d.o, src);
                 const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
-                const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
-                const float alpha = fminf(0.99f, ex * o);
-                const bool take = __builtin_amdgcn_inverse_ballot_w64(nb) & !(alpha < 1.0f / 255.0f);
-                // alphaBlend :59-67
-                const float aT = alpha * (1.0f - pc.w);
                 if (cfin) {  // uniform (see the dense event)
+                    const float ex = FAST_EXP ? __expf(p) : exp_defined_event<!GS_EV_SAFE>(p);
+                    const float alpha = fminf(0.99f, ex * o);
+                    const bool take = __builtin_amdgcn_inverse_ballot_w64(nb) & !(alpha < 1.0f / 255.0f);
+                    // alphaBlend :59-67
+                    const float aT = alpha * (1.0f - pc.w);
                     const float aZ = take ? aT : 0.0f;
                     pc.x = pc.x + r * aZ;
                     pc.y = pc.y + g * aZ;
                     pc.z = pc.z + bl * aZ;
                     pc.w = pc.w + aZ;
                 } else {
+                    const float ex = FAST_EXP ? __expf(p) : exp_defined_event(p);
+                    const float alpha = fminf(0.99f, ex * o);
+                    const bool take = __builtin_amdgcn_inverse_ballot_w64(nb) & !(alpha < 1.0f / 255.0f);
+                    const float aT = alpha * (1.0f - pc.w);
                     pc.x = take ? pc.x + r * aT : pc.x;
                     pc.y = take ? pc.y + g * aT : pc.y;
                     pc.z = take ? pc.z + bl * aT : pc.z;
@@ -1732,7 +1750,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // state by selects: the same bits when every colour of the batch is finite (the state's
         // channels are never -0, and x + (+-0) == x otherwise); a non-finite colour (inf * 0 is
         // NaN) keeps the selects.
-        cfin = ballot(!(__builtin_isfinite(Dc.x) & __builtin_isfinite(Dc.y) & __builtin_isfinite(Dc.z))) == 0;
+        bool ok = __builtin_isfinite(Dc.x) && __builtin_isfinite(Dc.y) && __builtin_isfinite(Dc.z);
+        if (GS_EV_SAFE) {  // ... and every power an event can see is finite and >= -80: the need test
+            // admits only p in [thr, 0] (NaN p only from non-finite or overflowing inputs, excluded
+            // here: |conic| < 1e20 and |mean| < 1e6 keep every product below 1e33)
+            ok = ok && (Dd.thr >= -80.0f) && (fabsf(Dd.mx) < 1.0e6f) && (fabsf(Dd.my) < 1.0e6f) &&
+                 (fabsf(Dd.a) < 1.0e20f) && (fabsf(Dd.b) < 1.0e20f) && (fabsf(Dd.c) < 1.0e20f);
+        }
+        cfin = ballot(!ok) == 0;
         if constexpr (SMALL) {
             blend_sparse(bk, Dd, Dc);
         } else {
@@ -1769,9 +1794,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             if (!step(std::integral_constant<int, 1>{})) break;
         }
     }
-    if (P.prefix && end < wend && !all_done && fr_h_totals) fr_h_totals[2] = 1u;  // (uniform) a prefix miss
-    // the depth this block's walk reached (the next frames' per-tile prefix targets)
-    if (P.depth && lane == 0) atomicMax(&P.depth[t], (uint32_t)max(0, min(base, end) - start));
+    const bool missed = P.prefix && end < wend && !all_done;  // (uniform) a prefix miss
+    if (missed && fr_h_totals) fr_h_totals[2] = 1u;
+    // the depth this block's walk reached (the next frames' per-tile prefix targets); a block that
+    // missed stopped at the cut, short of what it needs, and records its whole window instead, so
+    // the next frames keep that tile whole (up to the global target, which the miss doubles) --
+    // recording the reach at the cut kept the tile at that depth: under a moving camera every
+    // later frame missed again.  (The missed frame's re-render records the true depth too, but
+    // on another lane, unordered with the next frame's class selection.)
+    if (P.depth && lane == 0)
+        atomicMax(&P.depth[t], (uint32_t)max(0, missed ? wend - start : min(base, end) - start));
     if constexpr (SMALL) {  // the lane's pixel (coordinates again from the lane id, see below)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + (l2 & 7), qy = y0 + (l2 >> 3);

@@ -1,9 +1,9 @@
 // gs_util.hip -- measurement helpers of the C ABI (not on the frame path).
 //
 // gs_stream_copy_gbs: the HBM stream-copy rate of this GPU, measured in the same process as the
-// kernels it is compared with (bench.py's roofline.frac_of_copy): a float4 grid-stride copy
-// between two buffers far beyond the 256 MiB Infinity Cache, bytes read + written per second.
-// MI355X_MICROARCH.md quotes 6.29 TB/s for this pattern against the 8.0 TB/s spec.
+// kernels it is compared with (bench.py's roofline.frac_of_copy): a float4 copy (one per lane,
+// non-temporal) between two buffers far beyond the 256 MiB Infinity Cache, bytes read + written per second.
+// MI355X_MICROARCH.md quotes 6.29 TB/s for a float4 copy against the 8.0 TB/s spec.
 #include "gs_internal.hpp"
 
 #include <hip/hip_runtime.h>
@@ -13,19 +13,12 @@
 
 namespace {
 
-// 4 float4 per lane in flight per step: the loads of a step are issued before its stores
-__global__ __launch_bounds__(256) void k_stream_copy(const float4 *__restrict__ src, float4 *__restrict__ dst,
-                                                     size_t n4) {
-    const size_t stride = (size_t)gridDim.x * 256;
-    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < n4; i += stride) dst[i] = src[i];
+// one float4 per lane, non-temporal loads and stores (tools/micro/copy_bw.hip on MI355X, 1 GiB:
+// 6.58 TB/s; temporal 6.23; grid-stride loops of 4-8 float4 per lane 4.4-4.7; hipMemcpy 4.7)
+typedef float f4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_stream_copy(const f4v *__restrict__ src, f4v *__restrict__ dst, size_t n4) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n4) __builtin_nontemporal_store(__builtin_nontemporal_load(&src[i]), &dst[i]);
 }
 
 }  // namespace
@@ -35,7 +28,7 @@ extern "C" int gs_stream_copy_gbs(gs_ctx *ctx, size_t bytes, int reps, double *g
     if (!ctx) return gs::set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (int rc = gs_sync(ctx)) return rc;  // nothing of the ctx's frames shares the GPU with it
     const size_t n4 = bytes / 16;
-    float4 *a = nullptr, *b = nullptr;
+    f4v *a = nullptr, *b = nullptr;
     hipStream_t s = (hipStream_t)gs_stream(ctx);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     auto done = [&](int rc) {
@@ -50,8 +43,7 @@ extern "C" int gs_stream_copy_gbs(gs_ctx *ctx, size_t bytes, int reps, double *g
     if (hipMemsetAsync(a, 0, n4 * 16, s) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
         hipEventCreate(&e1) != hipSuccess)
         return done(gs::set_error(ctx, GS_ERR_HIP, "gs_stream_copy_gbs: setup failed"));
-    // 8 workgroups of 256 per CU (256 CUs): every CU keeps a full queue of loads in flight
-    const dim3 grid(256 * 8);
+    const dim3 grid((unsigned)((n4 + 255) / 256));
     std::vector<double> r;
     for (int i = 0; i < reps + 2; ++i) {
         const bool ab = (i & 1) == 0;  // alternate directions: neither buffer stays cached
