@@ -102,10 +102,12 @@ int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
  * GPURadixSort orders every entry, src/sort.cpp:139-203): each tile's list is sorted at least
  * `target` entries deep (default 32768; the blend reads ~2-20k of lists up to 0.8M long at
  * C3) and the rest of it is left unsorted.  Images are unchanged: a frame whose blend reaches
- * an unsorted position before saturating is rendered again with the full sort, and the target
- * doubles for the frames after it; after 64 frames in a row without a miss it halves again,
- * never below the configured target.  target 0: always the full sort.  Frames with fewer than
- * 64 * target entries (the previous frame's count) use the full sort.  Setting a target
+ * an unsorted position before saturating is rendered again with the full sort (alone, with any
+ * later frame in flight that writes the same output), and the target doubles for the frames after
+ * it; after 64 frames in a row without a miss it halves again, never below the configured target.
+ * Three misses within 32 prefix-sorted frames (a fast camera) turn the prefix sort off for the
+ * next 64 frames.  target 0: always the full sort.  Frames with fewer than
+ * 64 * target (the configured one) entries -- the previous frame's count -- use the full sort.  Setting a target
  * (>= 0) also clears the per-tile depths the blends recorded (a cold start).  Returns the
  * current target in *current when it is not NULL (with target < 0: only that). */
 int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current);

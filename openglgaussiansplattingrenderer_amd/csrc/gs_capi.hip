@@ -40,6 +40,8 @@ constexpr int kFusedMaxBlocks = 64;
 // itself, which costs a round trip per 64 tiles of 4096 entries)
 constexpr int64_t kSmallSortEntries = 512 << 10;
 // per-tile prefix depths from the blends' reach (gs::PrefixDev::depth); 0: the configured target everywhere
+constexpr uint64_t kPrefixMissWindow = 32;  // (three misses within it)
+constexpr int kPrefixCooldown = 64;
 #ifndef GS_PREFIX_DEPTH
 #define GS_PREFIX_DEPTH 1
 #endif
@@ -156,6 +158,14 @@ struct gs_ctx {
     // a prefix miss was seen: the next prefix-sorted frame sizes its passes 1-3 for every entry (the
     // tiles that missed now keep whole windows, so the kept count can jump past the last one)
     bool prefix_after_miss = false;
+    // misses close together (a fast camera: the per-tile depths lag the lists) cost more in
+    // re-rendered frames than the prefix sort saves (a re-render ~1.2 ms, the saving ~0.12 ms per
+    // frame at C3): kPrefixMissBurst misses within kPrefixMissWindow prefix-sorted frames turn the
+    // prefix sort off for the next kPrefixCooldown frames (a cold depth table's first frames miss
+    // once or twice while the depths settle; those do not)
+    uint64_t prefix_seen = 0;                    // prefix-sorted frames retired
+    uint64_t prefix_miss_at[2] = {~0ull, ~0ull}; // ... counts at the two misses before the newest
+    int prefix_cooldown = 0;
     uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
     int prefix_kept_target = 0;  // the depth the frame of prefix_kept was sorted to
     // the blend's sub-block form (gs_ctx_set_draw_sub): 0 by the frame's entry count, 8 or 16
@@ -360,22 +370,93 @@ int oldest_used(const gs_ctx *ctx, uint64_t seq_limit) {
     return k;
 }
 
-// A speculative frame's entries exceeded its capacity (emission dropped the excess, so its
-// image is wrong).  Every frame still in flight is complete after the sync; the speculative
-// ones are the newest (every host-synchronous operation validates first), so grow the entry
-// buffers and render them again, in order, through the synchronous path.
-int handle_overflow(gs_ctx *ctx) {
+// A completed speculative frame (slot k): its counts from the pinned ring, the prefix sort's
+// bookkeeping.  Returns true when the frame must be rendered again -- its entries exceeded the
+// capacity (the emission dropped the excess), a prefix-sorted blend reached an unsorted position
+// (miss) or the frame kept more entries than its sort passes could hold (full), or a fused
+// frame's look-back gave up -- with *need = the entries it needs; else the frame's counts become
+// the context's newest.
+bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
+    const gs_ctx::Slot &sl = ctx->slot[k];
+    const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
+    // a prefix-sorted frame whose blend reached an unsorted position: render it again
+    // (full sort) and sort deeper from now on
+    const uint32_t flag = ctx->h_ring[4 * k + 2];
+    const bool miss = sl.prefix && flag == 1u;
+    // ... or a fused frame (k_pre_emit) whose look-back wait gave up: its entries were
+    // placed from partial offsets (render it again; the depth stays)
+    const bool lb_fail = sl.fused && flag == 2u;
+    // ... or that kept more entries than its sort passes could hold (sized from earlier frames)
+    const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
+    if (sl.prefix) {
+        ctx->prefix_kept = ctx->h_ring[4 * k + 3];
+        ctx->prefix_kept_target = sl.target;
+        ctx->prefix_E = (uint64_t)(V + D);
+    }
+    if (miss) {
+        ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
+        ctx->prefix_clean_run = 0;
+        ctx->prefix_after_miss = true;
+        if (ctx->prefix_miss_at[0] != ~0ull && ctx->prefix_seen - ctx->prefix_miss_at[0] < kPrefixMissWindow) {
+            ctx->prefix_cooldown = kPrefixCooldown;
+            ctx->prefix_miss_at[0] = ctx->prefix_miss_at[1] = ~0ull;
+        } else {
+            ctx->prefix_miss_at[0] = ctx->prefix_miss_at[1];
+            ctx->prefix_miss_at[1] = ctx->prefix_seen;
+        }
+    } else if (++ctx->prefix_clean_run >= kPrefixDecay) {  // (prefix-sorted or not: a depth that
+        // a miss doubled comes down again)
+        ctx->prefix_clean_run = 0;
+        if (ctx->prefix_target > ctx->prefix_base)
+            ctx->prefix_target = std::max(ctx->prefix_base, ctx->prefix_target / 2);
+    }
+    if (miss || full) ctx->prefix_redo += 1;
+    if (sl.prefix) ctx->prefix_seen += 1;
+    if (sl.prefix && !miss && !full && sl.cap_sel >= (uint32_t)sl.cap) ctx->prefix_after_miss = false;
+    if (lb_fail) ctx->lb_redo += 1;
+    // the split layout of a fused frame holds its duplicates from index n on
+    *need = sl.fused ? (int64_t)sl.n + D : V + D;
+    if (*need > sl.cap || miss || full || lb_fail) return true;
+    ctx->V = V;
+    ctx->D = D;
+    ctx->E = V + D;
+    ctx->e_known = true;
+    return false;
+}
+
+// The frame in slot `bad` (checked, needing `need0` entries) must be rendered again.  After the
+// sync every frame in flight is complete and the speculative ones are the newest (every
+// host-synchronous operation validates first): each is checked, oldest first; the ones that
+// failed are rendered again, in order, through the synchronous path with grown buffers, and so is
+// every later frame that writes an output (or the draw-stats buffer) a re-rendered frame writes,
+// since an output must be written in frame order.  The others stand as rendered: a prefix miss
+// re-renders one frame (and the frame three later that shares its texture), not every frame in
+// flight.
+int handle_overflow(gs_ctx *ctx, int bad, int64_t need0) {
     if (int rc = sync_lanes(ctx)) return rc;
     gs_ctx::Slot redo[kRing];
-    int nredo = 0;
-    int64_t need = 0;
+    const void *dirty[2 * kRing];
+    int nredo = 0, ndirty = 0;
+    int64_t need = need0;
     for (int k; (k = oldest_used(ctx, ~0ull)) >= 0;) {
         gs_ctx::Slot &sl = ctx->slot[k];
-        if (sl.spec) {
-            redo[nredo++] = sl;
-            need = std::max<int64_t>(need, (int64_t)ctx->h_ring[4 * k] + ctx->h_ring[4 * k + 1]);
+        int64_t nk = 0;
+        bool again = k == bad;
+        if (!again && sl.spec) {
+            again = check_spec(ctx, k, &nk);
+            for (int i = 0; i < ndirty && !again; ++i)
+                again = dirty[i] == sl.out || (sl.draw_stats && dirty[i] == ctx->draw_stats);
+            if (again) nk = std::max<int64_t>(nk, ctx->h_ring[4 * k] + ctx->h_ring[4 * k + 1]);
         }
-        sl.used = false;  // the dropped frames' timings are not accumulated
+        if (again) {
+            redo[nredo++] = sl;
+            need = std::max(need, nk);
+            dirty[ndirty++] = sl.out;
+            if (sl.draw_stats) dirty[ndirty++] = ctx->draw_stats;
+        } else {
+            accumulate(ctx, k);
+        }
+        sl.used = false;  // (the re-rendered frames' timings are not accumulated)
     }
     if (int rc = ensure_entries(ctx, need)) return rc;
     for (int i = 0; i < nredo; ++i)
@@ -394,43 +475,8 @@ int retire_upto(gs_ctx *ctx, uint64_t seq_limit) {
             if (ctx->in_render)
                 ctx->acc.ms_host_wait += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
         }
-        if (sl.spec) {
-            const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
-            // a prefix-sorted frame whose blend reached an unsorted position: render it again
-            // (full sort) and sort deeper from now on
-            const uint32_t flag = ctx->h_ring[4 * k + 2];
-            const bool miss = sl.prefix && flag == 1u;
-            // ... or a fused frame (k_pre_emit) whose look-back wait gave up: its entries were
-            // placed from partial offsets (render it again; the depth stays)
-            const bool lb_fail = sl.fused && flag == 2u;
-            // ... or that kept more entries than its sort passes could hold (sized from earlier frames)
-            const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
-            if (sl.prefix) {
-                ctx->prefix_kept = ctx->h_ring[4 * k + 3];
-                ctx->prefix_kept_target = sl.target;
-                ctx->prefix_E = (uint64_t)(V + D);
-            }
-            if (miss) {
-                ctx->prefix_target = (int)std::min<int64_t>((int64_t)ctx->prefix_target * 2, 1 << 30);
-                ctx->prefix_clean_run = 0;
-                ctx->prefix_after_miss = true;
-            } else if (++ctx->prefix_clean_run >= kPrefixDecay) {  // (prefix-sorted or not: a depth that
-                // turned the prefix sort off, E < 64 * target, comes down again too)
-                ctx->prefix_clean_run = 0;
-                if (ctx->prefix_target > ctx->prefix_base)
-                    ctx->prefix_target = std::max(ctx->prefix_base, ctx->prefix_target / 2);
-            }
-            if (miss || full) ctx->prefix_redo += 1;
-            if (sl.prefix && !miss && !full && sl.cap_sel >= (uint32_t)sl.cap) ctx->prefix_after_miss = false;
-            // the split layout of a fused frame holds its duplicates from index n on
-            const int64_t need = sl.fused ? (int64_t)sl.n + D : V + D;
-            if (lb_fail) ctx->lb_redo += 1;
-            if (need > sl.cap || miss || full || lb_fail) return handle_overflow(ctx);
-            ctx->V = V;
-            ctx->D = D;
-            ctx->E = V + D;
-            ctx->e_known = true;
-        }
+        int64_t need = 0;
+        if (sl.spec && check_spec(ctx, k, &need)) return handle_overflow(ctx, k, need);
         accumulate(ctx, k);
         sl.used = false;
     }
@@ -1143,7 +1189,11 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     // prefix sort: frames of the size where the lists are long (the last observed count)
     // (enabled by the configured depth, not the doubled one: the per-tile depths keep what each
     // list needs, and a moving camera's occasional misses must not turn the prefix sort off)
-    const bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_base;
+    bool prefix = ctx->prefix_target > 0 && ctx->E >= (int64_t)64 * ctx->prefix_base;
+    if (ctx->prefix_cooldown > 0) {  // (misses close together: the full sort for a while)
+        ctx->prefix_cooldown -= 1;
+        prefix = false;
+    }
     gs::PrefixDev pd{};
     if (prefix) {
         if (!ctx->L->pre_buf) {
@@ -1378,6 +1428,9 @@ int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
     if (target >= 0) {
         ctx->prefix_base = ctx->prefix_target = target;
         ctx->prefix_clean_run = 0;
+        ctx->prefix_cooldown = 0;
+        ctx->prefix_miss_at[0] = ctx->prefix_miss_at[1] = ~0ull;
+        ctx->prefix_after_miss = false;
         if (ctx->prefix_depth) {  // a new target starts from a cold per-tile depth table (after the
             // frames in flight, whose blends write it)
             if (int rc = use_device(ctx)) return rc;

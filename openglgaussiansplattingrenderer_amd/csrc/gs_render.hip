@@ -1640,11 +1640,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             const float o = rl(d.o, src);
             const float r = rl(c.x, src), g = rl(c.y, src), bl = rl(c.z, src);
             uint32_t sat = 0;  // max bits of the w written (w >= 0: ordered as the floats)
-            auto event = [&](uint32_t e) {
-                // straight line: the pixel's state is loaded with the event, before the exp
-                const uint32_t pix = s_epix[e];
-                const float power = s_epow[GS_DRAW_POWPIX ? pix : e];
-                float4 col = s_col[pix];
+            // one event's blend (draw.glsl:118-134 on the pixel's state)
+            auto blend_ev = [&](float power, float4 col) __attribute__((always_inline)) {
                 if (cfin) {  // uniform: finite colours -- adding rgb * 0 leaves the state as it is
                     // (and, GS_EV_SAFE, every event's power in [-80, 0]: no underflow select)
                     const float ex = FAST_EXP ? __expf(power) : exp_defined_event<!GS_EV_SAFE>(power);
@@ -1669,6 +1666,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                     col.z = take ? col.z + bl * aT : col.z;
                     col.w = take ? col.w + aT : col.w;
                 }
+                return col;
+            };
+            auto event = [&](uint32_t e) {
+                // straight line: the pixel's state is loaded with the event, before the exp
+                const uint32_t pix = s_epix[e];
+                const float power = s_epow[GS_DRAW_POWPIX ? pix : e];
+                const float4 col = blend_ev(power, s_col[pix]);
                 s_col[pix] = col;
                 sat = max(sat, __float_as_uint(col.w));  // :129-133
             };
