@@ -91,7 +91,10 @@ struct PrefixDev {
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };
-constexpr uint32_t kPrefixDepthSlack = 4096;
+#ifndef GS_PREFIX_SLACK
+#define GS_PREFIX_SLACK 4096
+#endif
+constexpr uint32_t kPrefixDepthSlack = GS_PREFIX_SLACK;
 constexpr uint32_t kKey1Bits = 0x3f800000u;    // bits(1.0f)
 constexpr uint32_t kKey256Bits = 0x43800000u;  // bits(256.0f)
 // key class: t for the keys in [t, t+1), t < 256; 256 for every other bit pattern
