@@ -411,6 +411,12 @@ bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
             ctx->prefix_target = std::max(ctx->prefix_base, ctx->prefix_target / 2);
     }
     if (miss || full) ctx->prefix_redo += 1;
+#ifdef GS_PREFIX_TRACE  // (diagnostic builds: tools/diag/prefix_sweep.py)
+    if (sl.prefix)
+        fprintf(stderr, "prefix seen %llu miss %d full %d kept %u cap_sel %u target %d cooldown %d E %lld\n",
+                (unsigned long long)ctx->prefix_seen, (int)miss, (int)full, ctx->h_ring[4 * k + 3], sl.cap_sel,
+                ctx->prefix_target, ctx->prefix_cooldown, (long long)(V + D));
+#endif
     if (sl.prefix) ctx->prefix_seen += 1;
     if (sl.prefix && !miss && !full && sl.cap_sel >= (uint32_t)sl.cap) ctx->prefix_after_miss = false;
     if (lb_fail) ctx->lb_redo += 1;

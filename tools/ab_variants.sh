@@ -16,7 +16,7 @@ for round in 1 2; do
 import json; d=json.load(open('gpurun_out/ab_${v}_$round.json')); fr=d['frame']
 print('$v r$round fps %.1f' % d['value'], 'serial', fr['serial_ms_per_frame'], 'stages', fr['stage_ms'], 'draw1', d['roofline']['avg_launch_ms'])
 sw = fr.get('camera_sweep')
-if sw: print('   sweep', {k: (v['prefix']['frames_per_s'], v['prefix']['rendered_again'], v['prefix']['prefix_frames'], v['full_sort']['frames_per_s']) for k, v in sw.items() if isinstance(v, dict)})"
+if sw: print('   sweep', {k: (v['prefix']['frames_per_s'], v['prefix']['rendered_again'], v['prefix']['prefix_frames'], v['full_sort']['frames_per_s'], v.get('static_same_poses_fps')) for k, v in sw.items() if isinstance(v, dict)})"
   done
 done
 cp /tmp/libgsplat_hip.orig.so $L/libgsplat_hip.so
