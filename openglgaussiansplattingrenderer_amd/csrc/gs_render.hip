@@ -1242,6 +1242,20 @@ static_assert(sizeof(SurvLoad) == sizeof(SplatDraw), "SurvLoad mirrors SplatDraw
 #ifndef GS_EV_SAFE
 #define GS_EV_SAFE 1
 #endif
+// the blend's pixel states lane-major in LDS (see k_draw's qbase)
+#ifndef GS_DRAW_LANEMAJOR
+#define GS_DRAW_LANEMAJOR 1
+#endif
+// a state slot's pixel in the sub-block: lane-major slot 64 k + l holds (2 (l % 8) + k % 2,
+// 2 (l / 8) + k / 2); row-major slots and the SMALL form's pixel ids are 16 y + x
+template <bool SMALL>
+__device__ __forceinline__ int slot_x(uint32_t s) {
+    return (SMALL || !GS_DRAW_LANEMAJOR) ? (int)(s & 15u) : (int)(2u * (s & 7u) + ((s >> 6) & 1u));
+}
+template <bool SMALL>
+__device__ __forceinline__ int slot_y(uint32_t s) {
+    return (SMALL || !GS_DRAW_LANEMAJOR) ? (int)(s >> 4) : (int)(2u * ((s >> 3) & 7u) + (s >> 7));
+}
 #ifndef GS_DRAW_BATCH
 #define GS_DRAW_BATCH 32
 #endif
@@ -1341,9 +1355,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int qmax = max(E - 1, 0);
     // pixels outside the image count as done
     bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
+#if GS_DRAW_LANEMAJOR
+    // the pixel states are lane-major: the state of the lane's value k (pixel (pxa + k % 2,
+    // pya + k / 2)) is slot 64 k + lane -- a value's events, taken in lane order, read and write
+    // states 16 B apart (fewer LDS bank conflicts than the row-major pixel order)
+    const uint32_t qbase = (uint32_t)lane;
+    constexpr uint32_t kQuad[4] = {0u, 64u, 128u, 192u};
+#else
     // pixel ids are row-major in the sub-block (16 * y + x): the lane's quad is qbase + kQuad[k]
     const uint32_t qbase = 32u * ((uint32_t)lane >> 3) + 2u * ((uint32_t)lane & 7u);
     constexpr uint32_t kQuad[4] = {0u, 1u, 16u, 17u};
+#endif
     if constexpr (!SMALL) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1404,8 +1426,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         wave_lds_sync();
         spix = s_epix[min((uint32_t)lane, nact - 1)];
         SA = nact >= 64 ? ~0ull : ((1ull << nact) - 1);
-        const float sfx = (float)(x0 + (int)(spix & 15u));
-        const float sfy = (float)(y0 + (int)(spix >> 4));
+        const float sfx = (float)(x0 + slot_x<SMALL>(spix));
+        const float sfy = (float)(y0 + slot_y<SMALL>(spix));
         float mnx = sfx, mxx = sfx, mny = sfy, mxy = sfy;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1603,10 +1625,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             // v_mbcnt); each pixel occurs at most once, so the events are independent.  The
             // writes are exec-masked by the uniform event masks themselves (inverse ballot).
 #if GS_DRAW_POWPIX
-            // the powers go to their pixels' slots (every lane, two 8-byte stores, no address
-            // arithmetic); the compaction lists only the event pixels
+            // the powers go to their pixels' slots (every lane, no address arithmetic); the
+            // compaction lists only the event pixels
+#if GS_DRAW_LANEMAJOR
+            s_epow[qbase] = p00;
+            s_epow[qbase + 64u] = p10;
+            s_epow[qbase + 128u] = p01;
+            s_epow[qbase + 192u] = p11;
+#else
             *reinterpret_cast<float2 *>(&s_epow[qbase]) = make_float2(p00, p10);
             *reinterpret_cast<float2 *>(&s_epow[qbase + 16u]) = make_float2(p01, p11);
+#endif
 #endif
             if (__builtin_amdgcn_inverse_ballot_w64(b0)) {
                 const uint32_t e = below(b0, 0);
@@ -1695,8 +1724,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             keep &= ~ballot(ellipse_misses_rect(d.mx, d.my, d.a, d.b, d.c, d.thr, rx0, rx1, ry0, ry1));
         if (STATS) st_surv += __popcll(keep);
         if (!keep) return;  // uniform
-        const float sfx = (float)(x0 + (int)(spix & 15u));
-        const float sfy = (float)(y0 + (int)(spix >> 4));
+        const float sfx = (float)(x0 + slot_x<SMALL>(spix));
+        const float sfy = (float)(y0 + slot_y<SMALL>(spix));
         uint64_t km = all_done ? 0ull : keep;  // single-exit loop, as in blend_dense
         if (km) do {
             const int src = __builtin_ctzll(km);
@@ -1820,12 +1849,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
        // spilled there, a private segment in the dominant kernel)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + 2 * (l2 & 7), qy = y0 + 2 * (l2 >> 3);
-        const int qb = 32 * (l2 >> 3) + 2 * (l2 & 7);
+#if GS_DRAW_LANEMAJOR
+        const int qb = l2, q1 = 64, q2 = 128, q3 = 192;
+#else
+        const int qb = 32 * (l2 >> 3) + 2 * (l2 & 7), q1 = 1, q2 = 16, q3 = 17;
+#endif
         uint32_t *row0 = out + (size_t)qy * P.W + qx, *row1 = row0 + P.W;
         if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
-        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + 1]);
-        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + 16]);
-        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + 17]);
+        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + q1]);
+        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + q2]);
+        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
     }
     }
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
