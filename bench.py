@@ -295,21 +295,21 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
                          "prefix_frames": ps["frames"], "rendered_again": ps["redone"],
                          "kept_frac_last": round(ps["kept"] / max(1, ps["entries"]), 4),
                          "E_last": int(sp.stats.entries)}
-        # the same poses rendered static (warm depth table, 20 frames each at 5 poses along the pan):
+        # the same poses rendered static (warm depth table, 60 frames each at 5 poses along the pan):
         # the moving camera's frames/s against what those poses give without motion
         ctx.set_lanes(lanes)
         n_tot, t_tot = 0, 0.0
         for k in sorted({0, (steps - 1) // 4, (steps - 1) // 2, 3 * (steps - 1) // 4, steps - 1}):
             ctx.set_sort_prefix(base)
-            for _ in range(5):
+            for _ in range(10):
                 sp.render_uniforms(poses[k])
             ctx.sync()
             t0 = time.perf_counter()
-            for _ in range(20):
+            for _ in range(60):
                 sp.render_uniforms(poses[k])
             ctx.sync()
             t_tot += time.perf_counter() - t0
-            n_tot += 20
+            n_tot += 60
         st = n_tot / t_tot
         row["static_same_poses_fps"] = round(st, 2)
         for mode in ("prefix", "full_sort"):
@@ -317,7 +317,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
         out[f"{d:g}deg"] = row
     ctx.set_sort_prefix(base)
     out["source"] = ("host wall clock around the frames (gs_sync after the last); vs_static = frames/s over the "
-                     "static headline's value from the same run; static_same_poses_fps: 20 frames each of 5 poses along the "
+                     "static headline's value from the same run; static_same_poses_fps: 60 frames each of 5 poses along the "
                      "pan rendered without motion (prefix sort, warm depth table), frames over total time, and "
                      "vs_static_same_poses the sweep against it; cold_first_frame_ms: the first pose alone, one "
                      "lane, host wall clock around gs_render + gs_sync")
