@@ -298,7 +298,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
         # the same poses rendered static (warm depth table, 60 frames each at 5 poses along the pan):
         # the moving camera's frames/s against what those poses give without motion
         ctx.set_lanes(lanes)
-        n_tot, t_tot = 0, 0.0
+        n_tot, t_tot, per_pose = 0, 0.0, {}
         for k in sorted({0, (steps - 1) // 4, (steps - 1) // 2, 3 * (steps - 1) // 4, steps - 1}):
             ctx.set_sort_prefix(base)
             for _ in range(10):
@@ -308,10 +308,13 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
             for _ in range(60):
                 sp.render_uniforms(poses[k])
             ctx.sync()
-            t_tot += time.perf_counter() - t0
+            dt = time.perf_counter() - t0
+            per_pose[f"{d * k:g}deg"] = round(60 / dt, 1)
+            t_tot += dt
             n_tot += 60
         st = n_tot / t_tot
         row["static_same_poses_fps"] = round(st, 2)
+        row["static_per_pose_fps"] = per_pose
         for mode in ("prefix", "full_sort"):
             row[mode]["vs_static_same_poses"] = round(row[mode]["frames_per_s"] / st, 4)
         out[f"{d:g}deg"] = row

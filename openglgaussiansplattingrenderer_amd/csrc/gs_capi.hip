@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -45,6 +46,20 @@ constexpr int kPrefixCooldown = 64;
 #ifndef GS_PREFIX_DEPTH
 #define GS_PREFIX_DEPTH 1
 #endif
+// a turn of more than GS_PREFIX_TURN_MDEG millidegrees between consecutive frames makes a frame's
+// prefix selection ignore the per-tile depths
+#ifndef GS_PREFIX_TURN_MDEG
+#define GS_PREFIX_TURN_MDEG 250
+#endif
+const float kPrefixTurnCos = (float)std::cos(GS_PREFIX_TURN_MDEG * 1e-3 * 3.14159265358979323846 / 180.0);
+// cos of the rotation between two view matrices: (trace(R1^T R2) - 1) / 2 over their upper-left
+// 3x3 blocks (the same index set in either storage order)
+static float turn_cos(const float *a, const float *b) {
+    float tr = 0.0f;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) tr += a[4 * c + r] * b[4 * c + r];
+    return 0.5f * (tr - 1.0f);
+}
 
 // A frame lane: a stream and the per-frame buffers of the frames it runs.  Consecutive frames
 // alternate between the ctx's lanes (two by default), so frame k+1's preprocess, emission and
@@ -133,6 +148,7 @@ struct gs_ctx {
         int n = 0;
         uint32_t cap_sel = 0;  // prefix-sorted: the kept entries its sort passes 1-3 could hold
         int target = 0;        // prefix-sorted: its depth
+        bool turned = false;   // prefix-sorted without the per-tile depths (PrefixDev::use_depth 0)
     };
     Slot slot[kRing];
     hipEvent_t ev[kRing][kEv] = {};
@@ -166,6 +182,9 @@ struct gs_ctx {
     uint64_t prefix_seen = 0;                    // prefix-sorted frames retired
     uint64_t prefix_miss_at[2] = {~0ull, ~0ull}; // ... counts at the two misses before the newest
     int prefix_cooldown = 0;
+    float prev_view[16] = {};  // the newest frame's view matrix (the prefix sort's turn test)
+    bool prefix_kept_turned = false;  // prefix_kept came from a frame selected without the depths
+    bool have_prev_view = false;
     uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
     int prefix_kept_target = 0;  // the depth the frame of prefix_kept was sorted to
     // the blend's sub-block form (gs_ctx_set_draw_sub): 0 by the frame's entry count, 8 or 16
@@ -391,6 +410,7 @@ bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
     if (sl.prefix) {
         ctx->prefix_kept = ctx->h_ring[4 * k + 3];
         ctx->prefix_kept_target = sl.target;
+        ctx->prefix_kept_turned = sl.turned;
         ctx->prefix_E = (uint64_t)(V + D);
     }
     if (miss) {
@@ -1220,14 +1240,21 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
                                  ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
                                  : (int64_t)ctx->prefix_kept;
-        pd.cap_sel = (uint32_t)(ctx->prefix_kept && !ctx->prefix_after_miss ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
-                                                                              : cap_e);
         pd.target = (uint32_t)ctx->prefix_target;
         if (!ctx->prefix_depth) {  // (zeroed before any frame can read it)
             GS_HIP(ctx, hipMalloc(&ctx->prefix_depth, 256 * 4));
             GS_HIP(ctx, hipMemset(ctx->prefix_depth, 0, 256 * 4));
         }
         pd.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;
+        // a camera that turned more than kPrefixTurnDeg since the frame before: the recorded
+        // depths describe another view (their tiles' contents moved), so this frame's lists are
+        // kept to the configured target instead (a fast pan missed on nearly every frame)
+        pd.use_depth = ctx->have_prev_view && turn_cos(ctx->prev_view, u->view) < kPrefixTurnCos ? 0 : 1;
+        // (a kept count of the other selection -- with / without the depths -- does not size this one)
+        const bool same_sel = ctx->prefix_kept_turned == (pd.use_depth == 0);
+        pd.cap_sel = (uint32_t)(ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
+                                    ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
+                                    : cap_e);
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
     }
@@ -1252,6 +1279,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     if (prefix) {
         sl.cap_sel = pd.cap_sel;
         sl.target = ctx->prefix_target;
+        sl.turned = pd.use_depth == 0;
         pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
         sl.prefix = true;
         ctx->prefix_frames += 1;
@@ -1369,9 +1397,17 @@ int render_impl(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
                 int out_on_device, gs_frame_stats *stats) {
     // no stats wanted, output on the device, an entry count seen before: enqueue the whole
     // frame without a host round trip (validated at gs_sync / the next readback)
+    // (the prefix sort's turn test compares a frame's view with the frame before it)
+    auto seen = [&](int rc) {
+        if (rc == GS_OK) {
+            std::memcpy(ctx->prev_view, u->view, sizeof(ctx->prev_view));
+            ctx->have_prev_view = true;
+        }
+        return rc;
+    };
     if (!stats && out_on_device && ctx->e_known && !(flags & GS_FLAG_TIMING))
-        return render_spec(ctx, scene, u, flags, out_rgba8);
-    if (int rc = render_sync(ctx, scene, u, flags, out_rgba8, out_on_device, stats)) return rc;
+        return seen(render_spec(ctx, scene, u, flags, out_rgba8));
+    if (int rc = seen(render_sync(ctx, scene, u, flags, out_rgba8, out_on_device, stats))) return rc;
     if (flags & GS_FLAG_TIMING) {
         hipEvent_t *e = ctx->ev[ctx->cur];
         GS_HIP(ctx, hipEventSynchronize(e[8]));
@@ -1437,6 +1473,7 @@ int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
         ctx->prefix_cooldown = 0;
         ctx->prefix_miss_at[0] = ctx->prefix_miss_at[1] = ~0ull;
         ctx->prefix_after_miss = false;
+        ctx->prefix_kept = 0;  // (passes 1-3 of the next prefix-sorted frame sized for every entry)
         if (ctx->prefix_depth) {  // a new target starts from a cold per-tile depth table (after the
             // frames in flight, whose blends write it)
             if (int rc = use_device(ctx)) return rc;

@@ -88,6 +88,8 @@ struct PrefixDev {
     // (k_draw's atomicMax; decayed by 1/16 here each frame), or null.  A tile's target is then
     // min(target, 2 * depth + kPrefixDepthSlack): lists the blends read shallowly keep less.
     uint32_t *depth;
+    int32_t use_depth;  // 0: this frame's selection ignores the depths (the camera turned since the
+                        // frame before: they describe another view); its blend still records them
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };

@@ -1082,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t c = blockIdx.x, j = threadIdx.x;
     static_assert(kB == 8, "prefix_slot puts bucket 8j + k at word k * (kPrefixBuckets / 8) + j");
     uint32_t v[kB] = {};
-    const uint32_t dep = pre.depth ? pre.depth[c] : 0u;
+    const uint32_t dep = (pre.depth && pre.use_depth) ? pre.depth[c] : 0u;
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;

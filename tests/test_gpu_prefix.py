@@ -305,3 +305,39 @@ def test_prefix_depth_follows_the_blend():
         render_sync(sp, pose(W, H, k), ref)
         assert np.array_equal(got[i], ref.download(np.uint8, W * H * 4)), f"frame {i} (pose {k})"
     ctx.close()
+
+
+def test_prefix_fast_pan_ignores_stale_depths():
+    """A camera turning 3 degrees per frame: the per-tile depths recorded one pose earlier describe
+    another view, so those frames select without them (the configured depth) -- no frame rendered
+    again (selected with the depths, the first three missed and turned the prefix sort off), and
+    every image bit-exact against the host-synchronous full sort."""
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+
+    def pan(k):
+        cam = g.main_camera(W, H)
+        cam.rotateRight(3.0 * k)
+        return cam.uniforms()
+
+    render_sync(sp, pan(0), ref)
+    assert ctx.set_sort_prefix() == 32768
+    for _ in range(4):  # static frames first: the depths are recorded, and used
+        render_spec(sp, pan(0), ref)
+    ctx.sync()
+    ctx.prefix_stats(reset=True)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    got = []
+    for k in range(1, 10):
+        render_spec(sp, pan(k), outs[(k - 1) % 3])
+        if k % 3 == 0:
+            ctx.sync()
+            got += [o.download(np.uint8, W * H * 4) for o in outs]
+    ps = ctx.prefix_stats()
+    assert ps["frames"] == 9 and ps["redone"] == 0, ps
+    for k in range(1, 10):
+        render_sync(sp, pan(k), ref)
+        assert np.array_equal(got[k - 1], ref.download(np.uint8, W * H * 4)), f"pose {k}"
+    ctx.close()
