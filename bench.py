@@ -254,23 +254,29 @@ def sort_bench_c3(ctx, sp, u, reps: int = 20, warm: int = 3):
 
 
 def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, static_fps: float,
-                 deltas=(0.5, 3.0)):
+                 motions=(("turn", 0.5), ("turn", 3.0), ("walk", 0.1))):
     """The reference's loop moves the camera every frame (main.cpp:52-89 calls getInput at :76,
     src/Camera.cpp:77-119).  Pose k = the static pose + rotateRight(delta * k): an interactive
-    (0.5 deg / frame) and a fast (3 deg / frame) pan, `steps` frames each on `lanes` frames in
-    flight, with the prefix sort (the per-tile depths carried from frame to frame) and with every
-    frame fully sorted; each run starts from a cold depth table, whose first frame is also timed
-    alone (one lane)."""
-    import openglgaussiansplattingrenderer_amd as g
+    (0.5 deg / frame) and a fast (3 deg / frame) pan, `steps` frames each, and moveForward(0.1 * k)
+    (the reference's key step), 40 frames; on `lanes` frames in flight, with the prefix sort (the
+    per-tile depths carried from frame to frame) and with every frame fully sorted; each run
+    starts from a cold depth table, whose first frame is also timed alone (one lane)."""
     base = ctx.set_sort_prefix()
     out = {}
-    for d in deltas:
+    for kind, d in motions:
+        n = steps if kind == "turn" else min(steps, 40)
         poses = []
-        for k in range(steps):
+        for k in range(n):
             cam = camera_for_rank(W, H, view)
-            cam.rotateRight(d * k)
+            if kind == "turn":
+                cam.rotateRight(d * k)
+            else:
+                cam.moveForward(d * k)
             poses.append(cam.uniforms())
-        row = {"deg_per_frame": d, "frames": steps, "pan_deg": round(d * (steps - 1), 2)}
+        if kind == "turn":
+            row = {"deg_per_frame": d, "frames": n, "pan_deg": round(d * (n - 1), 2)}
+        else:
+            row = {"units_per_frame": d, "frames": n, "walk_units": round(d * (n - 1), 2)}
         for mode, tgt in (("prefix", base), ("full_sort", 0)):
             ctx.set_sort_prefix(0)
             ctx.set_lanes(1)
@@ -290,7 +296,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
             ctx.sync()
             dt = time.perf_counter() - t0
             ps = ctx.prefix_stats()
-            row[mode] = {"frames_per_s": round(steps / dt, 2), "vs_static": round(steps / dt / static_fps, 4),
+            row[mode] = {"frames_per_s": round(n / dt, 2), "vs_static": round(n / dt / static_fps, 4),
                          "cold_first_frame_ms": round(first_ms, 4),
                          "prefix_frames": ps["frames"], "rendered_again": ps["redone"],
                          "kept_frac_last": round(ps["kept"] / max(1, ps["entries"]), 4),
@@ -299,7 +305,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
         # the moving camera's frames/s against what those poses give without motion
         ctx.set_lanes(lanes)
         n_tot, t_tot, per_pose = 0, 0.0, {}
-        for k in sorted({0, (steps - 1) // 4, (steps - 1) // 2, 3 * (steps - 1) // 4, steps - 1}):
+        for k in sorted({0, (n - 1) // 4, (n - 1) // 2, 3 * (n - 1) // 4, n - 1}):
             ctx.set_sort_prefix(base)
             for _ in range(10):
                 sp.render_uniforms(poses[k])
@@ -309,7 +315,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
                 sp.render_uniforms(poses[k])
             ctx.sync()
             dt = time.perf_counter() - t0
-            per_pose[f"{d * k:g}deg"] = round(60 / dt, 1)
+            per_pose[f"{d * k:g}{'deg' if kind == 'turn' else 'units'}"] = round(60 / dt, 1)
             t_tot += dt
             n_tot += 60
         st = n_tot / t_tot
@@ -317,7 +323,7 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
         row["static_per_pose_fps"] = per_pose
         for mode in ("prefix", "full_sort"):
             row[mode]["vs_static_same_poses"] = round(row[mode]["frames_per_s"] / st, 4)
-        out[f"{d:g}deg"] = row
+        out[f"{d:g}deg" if kind == "turn" else f"walk{d:g}"] = row
     ctx.set_sort_prefix(base)
     out["source"] = ("host wall clock around the frames (gs_sync after the last); vs_static = frames/s over the "
                      "static headline's value from the same run; static_same_poses_fps: 60 frames each of 5 poses along the "
