@@ -186,8 +186,7 @@ SORT_BIG_N = 64 << 20  # 64M pairs: 512 MB of (key, value), 1.28 GB with the alt
 def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
     """The same pair sort beyond the caches: 64M uniform 32-bit keys (HBM-resident), median of
     `reps` hipEvent-timed sorts; algorithmic bytes 68 B/key; counter-based bytes from
-    the committed rocprofv3 measurement (profiles/r03/sort_64M.txt: 83.4 B/key by FETCH_SIZE x2 +
-    WRITE_SIZE at this size, with the r02 gather calibration's reading of the counters)."""
+    the newest committed rocprofv3 collection of this sort (profiles/rNN/sort_64M_pmc.json)."""
     import openglgaussiansplattingrenderer_amd as g
     n = SORT_BIG_N
     rng = np.random.default_rng(64)
@@ -210,13 +209,21 @@ def sort_bench_big(ctx, reps: int = 8, warm: int = 2):
               and np.array_equal(keys[np.minimum(v_out, n - 1)], k_out)
               and np.all((k_out[1:] != k_out[:-1]) | (v_out[1:] > v_out[:-1])))
     med = float(np.median(ms))
-    b_counter = 83.4  # B/key, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this sort (profiles/r03/sort_64M.txt)
-    return dict(n=n, keys="uniform 32-bit, seeded", ms_pairs=round(med, 4), gkeys_per_s=round(n / med / 1e6, 2),
-                hbm_frac_algorithmic=round(68.0 * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                hbm_frac_counters=round(b_counter * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                counter_bytes_per_key=b_counter, sorted_ok=ok,
-                source="hipEvents around gs_sort_pairs_u32 (12 kernels); 68 B/key algorithmic, 83.4 B/key by "
-                       "counters (profiles/r03/sort_64M.txt)")
+    out = dict(n=n, keys="uniform 32-bit, seeded", ms_pairs=round(med, 4), gkeys_per_s=round(n / med / 1e6, 2),
+               hbm_frac_algorithmic=round(68.0 * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), sorted_ok=ok,
+               source="hipEvents around gs_sort_pairs_u32, median of %d; 68 B/key algorithmic" % reps)
+    # counter bytes per key of this sort, from the newest committed PMC collection of it
+    # (profiles/rNN/sort_64M_pmc.json: FETCH_SIZE x2 + WRITE_SIZE of one sort's kernels / n)
+    p = newest_profile("sort_64M_pmc.json")
+    if p:
+        try:
+            b = float(json.load(open(p))["counter_bytes_per_key"])
+            out["counter_bytes_per_key"] = round(b, 2)
+            out["hbm_frac_counters"] = round(b * n / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            out["counter_source"] = os.path.relpath(p, ROOT)
+        except Exception:
+            pass
+    return out
 
 
 def sort_bench_c3(ctx, sp, u, reps: int = 20, warm: int = 3):
@@ -253,18 +260,22 @@ def sort_bench_c3(ctx, sp, u, reps: int = 20, warm: int = 3):
                 source="hipEvents around gs_sort_pairs_u32 (12 kernels), median of %d; 68 B/key algorithmic" % reps)
 
 
-def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, static_fps: float,
+SWEEP_FRAMES = {"turn": 20, "walk": 40}  # fixed, whatever --steps is: every run measures the same poses
+
+
+def camera_sweep(ctx, sp, W: int, H: int, view: int, lanes: int, static_fps: float,
                  motions=(("turn", 0.5), ("turn", 3.0), ("walk", 0.1))):
     """The reference's loop moves the camera every frame (main.cpp:52-89 calls getInput at :76,
     src/Camera.cpp:77-119).  Pose k = the static pose + rotateRight(delta * k): an interactive
-    (0.5 deg / frame) and a fast (3 deg / frame) pan, `steps` frames each, and moveForward(0.1 * k)
-    (the reference's key step), 40 frames; on `lanes` frames in flight, with the prefix sort (the
-    per-tile depths carried from frame to frame) and with every frame fully sorted; each run
-    starts from a cold depth table, whose first frame is also timed alone (one lane)."""
+    (0.5 deg / frame: a 9.5 deg pan) and a fast (3 deg / frame: 57 deg) pan, 20 frames each, and
+    moveForward(0.1 * k) (the reference's key step), 40 frames -- the same poses whatever --steps
+    is; on `lanes` frames in flight, with the prefix sort (the per-tile depths carried from frame
+    to frame) and with every frame fully sorted; each run starts from a cold depth table, whose
+    first frame is also timed alone (one lane)."""
     base = ctx.set_sort_prefix()
     out = {}
     for kind, d in motions:
-        n = steps if kind == "turn" else min(steps, 40)
+        n = SWEEP_FRAMES[kind]
         poses = []
         for k in range(n):
             cam = camera_for_rank(W, H, view)
@@ -333,6 +344,44 @@ def camera_sweep(ctx, sp, W: int, H: int, view: int, steps: int, lanes: int, sta
     return out
 
 
+def cpp_facade(sp, W: int, H: int, frames: int, warmup: int, lanes: int, py_fps: float, py_serial_ms: float,
+               E_py: int):
+    """The kept C++ API (include/gsplat_splats.hpp) in the reference's own loop shape (main.cpp:40-89:
+    Camera, Splats(path, W, H), then per frame the pose update, Splats::gpuRender, display), built as
+    openglgaussiansplattingrenderer_amd/lib/gs_main_loop: the same scene written as a ply (raw fields,
+    tests/plyFileGenerator.py layout, scenes.write_raw_ply; the facade's loader activates it as
+    from_raw does) and loaded
+    through the three-argument constructor; frames one at a time (finish() per frame, as main.cpp
+    blocks on its timestamp query) and enqueued ahead on `lanes` lanes, host wall clock."""
+    import shutil
+    import subprocess
+    import tempfile
+    from openglgaussiansplattingrenderer_amd.scenes import BICYCLE_N, bicycle_standin_raw, write_raw_ply
+    exe = os.path.join(ROOT, "openglgaussiansplattingrenderer_amd", "lib", "gs_main_loop")
+    if not os.path.exists(exe) or sp.numSplats != BICYCLE_N or os.environ.get("GS_BICYCLE_PLY"):
+        return None
+    d = tempfile.mkdtemp(prefix="gs_facade_")
+    try:
+        means, f_dc, logit, log_sc, rot = bicycle_standin_raw(BICYCLE_N)
+        ply = os.path.join(d, "c3_standin.ply")
+        write_raw_ply(ply, means, f_dc, logit, log_sc, rot)
+        r = subprocess.run([exe, ply, str(W), str(H), str(frames), str(warmup), str(lanes)], capture_output=True,
+                           text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": (r.stdout + r.stderr)[-400:]}
+        out = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    out["E_matches_python"] = out.get("E") == E_py
+    out["ahead_vs_python_gs_render"] = round(out["ahead_fps"] / py_fps, 4)
+    out["serial_vs_python_one_lane"] = round(out["serial_fps"] / (1e3 / py_serial_ms), 4)
+    out["source"] = ("lib/gs_main_loop (apps/gs_main_loop.cpp): gs::Camera + gs::Splats(path, W, H) + gpuRender per "
+                     "frame + present(); serial = finish() after every frame; ahead = frames enqueued on the lanes, "
+                     "finish() after the last; host wall clock; compared with this run's Python gs_render value "
+                     "(same lanes) and one-lane serial_ms_per_frame")
+    return out
+
+
 def copy_peak(ctx, nbytes: int = 1 << 30, reps: int = 10):
     """stream-copy rate of this GPU in this run (gs_stream_copy_gbs: non-temporal float4 copy of
     1 GiB, one per lane, read + write bytes): the practical HBM ceiling beside the 8 TB/s spec"""
@@ -365,18 +414,31 @@ def cpu_baseline(sp, u, flags, budget_s: float = 20.0):
                 detail=r)
 
 
+def newest_profile(name: str):
+    """the newest round's committed collection of `name` (profiles/rNN/name), or None"""
+    import glob
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", name)))
+    return cands[-1] if cands else None
+
+
 def load_pmc(kernel: str, field: str = "hbm_bytes_per_launch"):
-    """From the committed rocprofv3 PMC summary (profiles/pmc_summary.json, tools/collect_profiles.sh):
-    HBM traffic per launch (FETCH_SIZE x2 for streams, x1 for the blend's calibrated gathers,
-    + WRITE_SIZE), or another field ("sq": the SQ counters per dispatch); None if absent."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(p):
+    """From the newest round's committed rocprofv3 PMC summary (profiles/rNN/pmc_summary.json,
+    `tools/gpu_run.sh profiles rNN`): HBM traffic per launch (FETCH_SIZE x2 for streams, x1 for
+    the blend's calibrated gathers, + WRITE_SIZE), or another field ("sq": the SQ counters per
+    dispatch); None if absent."""
+    p = newest_profile("pmc_summary.json")
+    if not p:
         return None
     try:
         d = json.load(open(p))
         return d.get(kernel, {}).get(field)
     except Exception:
         return None
+
+
+def pmc_source() -> str | None:
+    p = newest_profile("pmc_summary.json")
+    return os.path.relpath(p, ROOT) if p else None
 
 
 SIMDS = 1024            # 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
@@ -387,7 +449,7 @@ SHADER_ENGINES = 32     # SQ_BUSY_CYCLES is summed over them
 
 def issue_ceiling(kernel: str, launch_ms: float):
     """The blend is bound by vector-instruction issue, not HBM.  Two views from the SQ pass
-    (profiles/pmc_summary.json, same collection as the traffic):
+    (the newest profiles/rNN/pmc_summary.json, same collection as the traffic):
       * naive: SQ_INSTS_VALU at one wave64 VALU per SIMD every 2 cycles at 2.4 GHz -- a lower
         bound on the issue time, since most of the blend's instructions cost more than v_fma_f32
         (tools/micro/valu_cost.hip: v_readlane / v_cmp to an SGPR 1.7x, v_mbcnt / v_cndmask /
@@ -402,7 +464,7 @@ def issue_ceiling(kernel: str, launch_ms: float):
     ceil_ms = v * VALU_CYC / (SIMDS * CLOCK_GHZ * 1e9) * 1e3
     out = {"valu_insts_per_launch": v, "salu_insts_per_launch": sq.get("SQ_INSTS_SALU"),
            "ceiling_ms": round(ceil_ms, 4), "frac": round(ceil_ms / launch_ms, 4),
-           "source": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cyc / (1024 SIMDs x 2.4 GHz)"}
+           "source": "SQ_INSTS_VALU per launch (%s) x 2 cyc / (1024 SIMDs x 2.4 GHz)" % pmc_source()}
     act, busy = sq.get("SQ_ACTIVE_INST_VALU"), sq.get("SQ_BUSY_CYCLES")
     if act and busy:
         simd_cycles = float(busy) / SHADER_ENGINES * SIMDS
@@ -432,6 +494,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sort-bench", action="store_true")
     ap.add_argument("--no-sweep", action="store_true", help="skip the moving-camera frames (frame.camera_sweep)")
+    ap.add_argument("--no-facade", action="store_true", help="skip the C++ facade loop (frame.cpp_facade)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only (spawn / rendezvous / per-rank pose / barrier / gather), no GPU: "
@@ -585,7 +648,7 @@ def main():
                 "avg_launch_ms_source": ("hipEvents on the draw dispatch, frames one at a time (1 lane): the kernel "
                                          "alone on the GPU" if dom == "draw" else
                                          "hipEvents of the one-lane stage-timing pass"),
-                "traffic": load_pmc(kern_name)}
+                "traffic": load_pmc(kern_name), "traffic_source": pmc_source()}
     if dom == "draw":
         live = alg["draw"] / (draw_ms_live * 1e-3) / 1e9
         roofline["timed_region"] = {
@@ -606,7 +669,10 @@ def main():
 
     sweep = None
     if not args.no_sweep and args.config != "c2":
-        sweep = camera_sweep(ctx, sp, W, H, view, args.steps, args.lanes, value / world)
+        sweep = camera_sweep(ctx, sp, W, H, view, args.lanes, value / world)
+    facade = None
+    if not args.no_facade and rank == 0 and world == 1 and flags == 0 and args.config in ("c3", "c4"):
+        facade = cpp_facade(sp, W, H, args.steps, args.warmup, args.lanes, value, serial_ms, E)
     copy = copy_peak(ctx) if rank == 0 else None
     if copy:
         roofline["copy_peak_gbs"] = copy["gbs_median"]
@@ -658,6 +724,7 @@ def main():
                       "serial_draw_ms": round(tm_serial["ms_draw"] / max(1, tm_serial["frames"]), 4),
                       "prefix_sort": prefix,
                       "camera_sweep": sweep,
+                      "cpp_facade": facade,
                       "frame_bytes_algorithmic": int(frame_bytes),
                       "frame_hbm_frac_algorithmic": round(frame_frac, 4),
                       "frame_bytes_source": "40N + 24V (preprocess) + 8E (emission) + sort (4E + 16E + 48 kept "

@@ -218,6 +218,11 @@ int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t
               void *out_rgba8, int out_on_device, gs_frame_stats *stats);
 /* counts (num_splats, visible, duplicates, entries) of the newest frame; waits for it */
 int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats);
+/* the same counts of the newest frame whose counts the host has already seen, without waiting:
+ * behind gs_render's frames in flight by up to the number of lanes (the reference reads the count
+ * back each frame, src/Splats.cpp:579-583, stalling its pipeline; the C++ facade's gpuRender
+ * fills Splats::numDuplicates from this) */
+int gs_seen_stats(gs_ctx *ctx, gs_frame_stats *stats);
 
 /* stage-level entry points mirroring the reference's Splats methods */
 /* Splats::preprocess (src/Splats.cpp:542-585) + the per-splat entry emission.

@@ -171,7 +171,8 @@ class Splats {
         setup(filePath, width, height);
     }
     ~Splats() {
-        if (texture_) gs_free(ctx_->get(), texture_);
+        for (void *&t : textures_)
+            if (t) gs_free(ctx_->get(), t);
         gs_scene_destroy(scene_);
     }
     Splats(const Splats &) = delete;
@@ -187,27 +188,30 @@ class Splats {
     }
     void loadShaders() {}  // src/Splats.cpp:156-172: nothing to compile at run time
 
-    // src/Splats.cpp:587-597
+    // src/Splats.cpp:587-597.  One frame enqueued without a host round trip: gs_render of the
+    // uniforms into the back texture of a ring of kTextures (the newest frame's becomes
+    // texture()), no stats pointer, no glFinish -- the frame's entry count stays on the device and
+    // frames overlap on the context's lanes (Context::setLanes).  numDuplicates is the count of the
+    // newest frame the host has seen (gs_seen_stats: up to the lanes behind; the reference maps
+    // its atomic counter back every frame, stalling, src/Splats.cpp:579-583).  The stage methods
+    // below keep the reference's staged semantics (one readback per frame) for callers that use
+    // them one by one.  The frame is complete after Context::finish() or any readback.
     void gpuRender(const mat4 &viewMatrix, int width, int height, float focal_x, float focal_y, float tan_fov_x,
                    float tan_fov_y, const mat4 &vpMatrix) {
-        preprocess(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix);
-        computeBins();
-        sort();
-        ctx_->finish();
-        draw(width, height, float(width) / 16.f, float(height) / 16.f);
+        const gs_uniforms u = uniforms(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix);
+        void *back = backTexture(width, height);
+        if (report(gs_render(ctx_->get(), scene_, &u, flags_, back, 1, nullptr), ctx_->get()) < 0) return;
+        front_ = (front_ + 1) % kTextures;
+        texture_ = back;
+        width_ = width;
+        height_ = height;
+        gs_frame_stats st{};
+        if (gs_seen_stats(ctx_->get(), &st) == GS_OK) numDuplicates = (int)st.duplicates;
     }
     // src/Splats.cpp:542-585 (+ emission; the duplicate count is exact, not capped)
     void preprocess(const mat4 &viewMatrix, int width, int height, float focal_x, float focal_y, float tan_fov_x,
                     float tan_fov_y, const mat4 &vpMatrix) {
-        gs_uniforms u;
-        std::memcpy(u.view, viewMatrix.data(), sizeof(u.view));
-        std::memcpy(u.vp, vpMatrix.data(), sizeof(u.vp));
-        u.width = width;
-        u.height = height;
-        u.focal_x = focal_x;
-        u.focal_y = focal_y;
-        u.tan_fov_x = tan_fov_x;
-        u.tan_fov_y = tan_fov_y;
+        const gs_uniforms u = uniforms(viewMatrix, width, height, focal_x, focal_y, tan_fov_x, tan_fov_y, vpMatrix);
         gs_frame_stats st{};
         report(gs_preprocess(ctx_->get(), scene_, &u, flags_, &st), ctx_->get());
         numDuplicates = (int)st.duplicates;
@@ -225,11 +229,14 @@ class Splats {
         if (!sorted_) sort();
         report(gs_compute_bins(ctx_->get()), ctx_->get());
     }
-    // src/Splats.cpp:356-381
+    // src/Splats.cpp:356-381 (into the current texture)
     void draw(int width, int height, float tileWidth, float tileHeight) {
         ensureTexture(width, height);
         report(gs_draw(ctx_->get(), scene_, width, height, tileWidth, tileHeight, flags_, texture_, 1), ctx_->get());
     }
+    // the display step of main.cpp:72 (src/Splats.cpp:383-412 draws the texture on a quad): the
+    // device texture a presenter samples -- the newest frame's -- with no host work and no wait
+    const void *present() const { return texture_; }
     // src/Splats.cpp:383-412 presents the texture; headless: copy it to the host (row 0 = GL row 0)
     std::vector<uint8_t> display() const {
         std::vector<uint8_t> img((size_t)width_ * height_ * 4);
@@ -288,26 +295,163 @@ class Splats {
         report(gs_covariance3d(numSplats, &scales[0].x, &rotations[0].x, covarianceMatrices.data()));
         std::cout << "Finished computing covariance matrices" << std::endl;
     }
+    static gs_uniforms uniforms(const mat4 &viewMatrix, int width, int height, float focal_x, float focal_y,
+                                float tan_fov_x, float tan_fov_y, const mat4 &vpMatrix) {
+        gs_uniforms u;
+        std::memcpy(u.view, viewMatrix.data(), sizeof(u.view));
+        std::memcpy(u.vp, vpMatrix.data(), sizeof(u.vp));
+        u.width = width;
+        u.height = height;
+        u.focal_x = focal_x;
+        u.focal_y = focal_y;
+        u.tan_fov_x = tan_fov_x;
+        u.tan_fov_y = tan_fov_y;
+        return u;
+    }
+    // the ring's textures hold at least width x height pixels
+    bool sizeTextures(int width, int height) {
+        const size_t need = (size_t)width * height * 4;
+        if (need <= cap_) return true;
+        for (void *&t : textures_) {
+            if (t) gs_free(ctx_->get(), t);  // (gs_free waits for the frames in flight)
+            t = nullptr;
+        }
+        cap_ = 0;
+        texture_ = nullptr;
+        for (void *&t : textures_)
+            if (report(gs_malloc(ctx_->get(), need, &t), ctx_->get()) < 0) return false;
+        cap_ = need;
+        texture_ = textures_[front_];
+        return true;
+    }
+    // the staged path draws into the current texture
     void ensureTexture(int width, int height) {
-        if (texture_ && (size_t)width * height <= (size_t)width_ * height_) {
+        if (sizeTextures(width, height)) {
+            texture_ = textures_[front_];
             width_ = width;
             height_ = height;
-            return;
         }
-        if (texture_) gs_free(ctx_->get(), texture_);
-        texture_ = nullptr;
-        report(gs_malloc(ctx_->get(), (size_t)width * height * 4, &texture_), ctx_->get());
-        width_ = width;
-        height_ = height;
+    }
+    // gpuRender's output: the oldest texture of the ring (frames in flight write the others;
+    // gs_render orders blends into one output by frame)
+    void *backTexture(int width, int height) {
+        if (!sizeTextures(width, height)) return nullptr;
+        return textures_[(front_ + 1) % kTextures];
     }
 
+    // one texture per frame lane (up to three frames in flight): consecutive frames' blends
+    // write different outputs and so may overlap (double/triple buffering)
+    static constexpr int kTextures = 3;
     Context *ctx_ = nullptr;
     std::unique_ptr<Context> own_;  // created when no Context was current
     uint32_t flags_ = 0;
     gs_scene *scene_ = nullptr;
-    void *texture_ = nullptr;
+    void *textures_[kTextures] = {nullptr, nullptr, nullptr};
+    size_t cap_ = 0;   // bytes of each ring texture
+    int front_ = 0;    // ring index of the current texture
+    void *texture_ = nullptr;  // the current texture (the newest frame's)
     int width_ = 0, height_ = 0;
     bool sorted_ = false;
+};
+
+// glm operator*(mat4, mat4): column c = A[0] B[c][0] + A[1] B[c][1] + A[2] B[c][2] + A[3] B[c][3],
+// summed left to right (the order gs_camera_uniforms uses for main.cpp:64's vp)
+inline mat4 operator*(const mat4 &a, const mat4 &b) {
+    mat4 o{};
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r)
+            o.m[c][r] = a.m[0][r] * b.m[c][0] + a.m[1][r] * b.m[c][1] + a.m[2][r] * b.m[c][2] + a.m[3][r] * b.m[c][3];
+    return o;
+}
+
+// include/Camera.h:13-66 (src/Camera.cpp): the uniform generator of main.cpp's loop, with the
+// reference's quirks (tan of degrees in getTanFovx/y, focal x from fovy; gs_camera_update).
+// Movement follows src/Camera.cpp:77-119 (forward / left along the view matrix's rotation rows).
+class Camera {
+  public:
+    Camera() : Camera(0.f, 0.f, 0.f) {  // src/Camera.cpp:13
+        c_.near_plane = 0.0001f;
+        update();
+    }
+    Camera(float x, float y, float z) {
+        c_.position[0] = x;
+        c_.position[1] = y;
+        c_.position[2] = z;
+        c_.fovy = 60.0f;
+        c_.near_plane = 0.1f;
+        c_.far_plane = 10000.0f;
+        c_.width = 1024;
+        c_.height = 512;
+        update();
+    }
+    // every mutator recomputes the matrices, as the reference's call update() (src/Camera.cpp)
+    void rotateRight(float angle) {
+        c_.rotation[1] += angle;
+        update();
+    }
+    void rotateLeft(float angle) { rotateRight(-angle); }
+    void rotateUp(float angle) {
+        c_.rotation[0] += angle;
+        update();
+    }
+    void rotateDown(float angle) { rotateUp(-angle); }
+    void moveForward(float d) {
+        for (int k = 0; k < 3; ++k) c_.position[k] += view_.m[k][2] * d;
+        update();
+    }
+    void moveBackward(float d) { moveForward(-d); }
+    void moveLeft(float d) {
+        for (int k = 0; k < 3; ++k) c_.position[k] += view_.m[k][0] * d;
+        update();
+    }
+    void moveRight(float d) { moveLeft(-d); }
+    void moveUp(float d) {
+        c_.position[1] += d;
+        update();
+    }
+    void moveDown(float d) { moveUp(-d); }
+    void setWidthHeight(int width, int height) {
+        c_.width = width;
+        c_.height = height;
+        update();
+    }
+    void setPosition(float x, float y, float z) {
+        c_.position[0] = x;
+        c_.position[1] = y;
+        c_.position[2] = z;
+        update();
+    }
+    void setRotation(float x, float y, float z) {
+        c_.rotation[0] = x;
+        c_.rotation[1] = y;
+        c_.rotation[2] = z;
+        update();
+    }
+    void setFovy(float fovy) {
+        c_.fovy = fovy;
+        update();
+    }
+    // src/Camera.cpp:181-212: view, projection and the getters' values from the current pose
+    void update() { gs_camera_update(&c_, &view_.m[0][0], &proj_.m[0][0], &fx_, &fy_, &tanx_, &tany_); }
+    mat4 getViewMatrix() const { return view_; }
+    mat4 getProjectionMatrix() const { return proj_; }
+    float getFocalX() const { return fx_; }
+    float getFocalY() const { return fy_; }
+    float getTanFovx() const { return tanx_; }
+    float getTanFovy() const { return tany_; }
+    int getWidth() const { return c_.width; }
+    int getHeight() const { return c_.height; }
+    // the gpuRender arguments exactly as main.cpp:62-64 passes them (gs_camera_uniforms)
+    gs_uniforms uniforms() const {
+        gs_uniforms u{};
+        gs_camera_uniforms(&c_, &u);
+        return u;
+    }
+
+  private:
+    gs_camera c_{};
+    mat4 view_{}, proj_{};
+    float fx_ = 0.f, fy_ = 0.f, tanx_ = 0.f, tany_ = 0.f;
 };
 
 // Camera getters as main.cpp:62-64 passes them (src/Camera.cpp restatement)

@@ -141,6 +141,7 @@ SIGNATURES = {
     "gs_scene_count": (_i, [_vp]),
     "gs_render": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, _vp, _i, ctypes.POINTER(gs_frame_stats)]),
     "gs_last_stats": (_i, [_vp, _vp]),
+    "gs_seen_stats": (_i, [_vp, _vp]),
     "gs_preprocess": (_i, [_vp, _vp, ctypes.POINTER(gs_uniforms), _u32, ctypes.POINTER(gs_frame_stats)]),
     "gs_sort": (_i, [_vp]),
     "gs_compute_bins": (_i, [_vp]),

@@ -22,6 +22,10 @@
 // 4 sort start, 5 sort done, 6 bins done, 7 draw start, 8 draw done
 constexpr int kEv = 9;
 constexpr int kRing = 4;
+// pinned ring words per frame slot: [0] V, [1] D (k_scan_blocksums / k_pre_emit), [2] k_draw's
+// prefix-miss flag, [3] kept entries of a prefix-sorted frame, [4] k_pre_emit's look-back give-up
+// flag (a word of its own: a miss store cannot overwrite it)
+constexpr int kRingWords = 8;
 constexpr int kPrefixDecay = 64;  // frames without a prefix-sort miss before the depth halves
 // Frames with fewer entries than this, and at most kSmallDrawSubBlocks 16x16 sub-blocks, blend
 // in 8x8 sub-blocks (gs_ctx_set_draw_sub): their blend is latency-bound (~one wave per SIMD, the
@@ -90,6 +94,9 @@ struct Lane {
     uint32_t lb_cap = 0;  // status words per half
     int lb_par = 0;
     bool split = false;  // the newest frame's entries are in the split layout (k_pre_emit)
+    // the newest frame (GS_FLAG_SH, prefix-sorted) coloured only its kept entries' splats
+    // (k_sh_kept): a full re-sort for the stage calls colours every splat first (resort_full)
+    bool sh_partial = false;
     // the newest frame's scene and preprocess parameters (a split frame's readbacks preprocess it
     // again on the staged path, which also writes the emission records)
     const gs_scene *pe_scene = nullptr;
@@ -240,6 +247,12 @@ int use_device(gs_ctx *ctx) {
     return GS_OK;
 }
 
+}  // namespace
+
+int gs::ctx_use_device(gs_ctx *ctx) { return use_device(ctx); }
+
+namespace {
+
 // wait on the host for every lane (all of them: after gs_ctx_set_lanes lowered the count, the
 // newest frame and its non-frame work may sit on a lane beyond it)
 int sync_lanes(gs_ctx *ctx) {
@@ -332,7 +345,7 @@ gs::FrameDev frame_dev(gs_ctx *ctx) {
     f.rec = ctx->L->rec;
     f.blocksum = ctx->L->blocksum;
     f.totals = ctx->L->totals;
-    f.h_totals = ctx->h_ring_dev + 4 * ctx->cur;
+    f.h_totals = ctx->h_ring_dev + kRingWords * ctx->cur;
     f.col = ctx->L->col;
     return f;
 }
@@ -397,18 +410,17 @@ int oldest_used(const gs_ctx *ctx, uint64_t seq_limit) {
 // the context's newest.
 bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
     const gs_ctx::Slot &sl = ctx->slot[k];
-    const int64_t V = ctx->h_ring[4 * k], D = ctx->h_ring[4 * k + 1];
+    const int64_t V = ctx->h_ring[kRingWords * k], D = ctx->h_ring[kRingWords * k + 1];
     // a prefix-sorted frame whose blend reached an unsorted position: render it again
     // (full sort) and sort deeper from now on
-    const uint32_t flag = ctx->h_ring[4 * k + 2];
-    const bool miss = sl.prefix && flag == 1u;
+    const bool miss = sl.prefix && ctx->h_ring[kRingWords * k + 2] != 0u;
     // ... or a fused frame (k_pre_emit) whose look-back wait gave up: its entries were
     // placed from partial offsets (render it again; the depth stays)
-    const bool lb_fail = sl.fused && flag == 2u;
+    const bool lb_fail = sl.fused && ctx->h_ring[kRingWords * k + 4] != 0u;
     // ... or that kept more entries than its sort passes could hold (sized from earlier frames)
-    const bool full = sl.prefix && ctx->h_ring[4 * k + 3] > sl.cap_sel;
+    const bool full = sl.prefix && ctx->h_ring[kRingWords * k + 3] > sl.cap_sel;
     if (sl.prefix) {
-        ctx->prefix_kept = ctx->h_ring[4 * k + 3];
+        ctx->prefix_kept = ctx->h_ring[kRingWords * k + 3];
         ctx->prefix_kept_target = sl.target;
         ctx->prefix_kept_turned = sl.turned;
         ctx->prefix_E = (uint64_t)(V + D);
@@ -434,7 +446,7 @@ bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
 #ifdef GS_PREFIX_TRACE  // (diagnostic builds: tools/diag/prefix_sweep.py)
     if (sl.prefix)
         fprintf(stderr, "prefix seen %llu miss %d full %d kept %u cap_sel %u target %d cooldown %d E %lld\n",
-                (unsigned long long)ctx->prefix_seen, (int)miss, (int)full, ctx->h_ring[4 * k + 3], sl.cap_sel,
+                (unsigned long long)ctx->prefix_seen, (int)miss, (int)full, ctx->h_ring[kRingWords * k + 3], sl.cap_sel,
                 ctx->prefix_target, ctx->prefix_cooldown, (long long)(V + D));
 #endif
     if (sl.prefix) ctx->prefix_seen += 1;
@@ -460,10 +472,18 @@ bool check_spec(gs_ctx *ctx, int k, int64_t *need) {
 // flight.
 int handle_overflow(gs_ctx *ctx, int bad, int64_t need0) {
     if (int rc = sync_lanes(ctx)) return rc;
-    gs_ctx::Slot redo[kRing];
+    gs_ctx::Slot redo[kRing + 1];
     const void *dirty[2 * kRing];
     int nredo = 0, ndirty = 0;
     int64_t need = need0;
+    // the newest frame in flight: the context's readback state (counts, buffers, stage) must be
+    // its own after the re-renders, so it is rendered again last if it stood (a
+    // re-render of an older frame alone left gs_last_stats / gs_frame_read on that older frame)
+    int newest = -1;
+    for (int i = 0; i < kRing; ++i)
+        if (ctx->slot[i].used && (newest < 0 || ctx->slot[i].seq > ctx->slot[newest].seq)) newest = i;
+    const gs_ctx::Slot newest_sl = newest >= 0 ? ctx->slot[newest] : gs_ctx::Slot{};
+    bool newest_redone = false;
     for (int k; (k = oldest_used(ctx, ~0ull)) >= 0;) {
         gs_ctx::Slot &sl = ctx->slot[k];
         int64_t nk = 0;
@@ -472,17 +492,24 @@ int handle_overflow(gs_ctx *ctx, int bad, int64_t need0) {
             again = check_spec(ctx, k, &nk);
             for (int i = 0; i < ndirty && !again; ++i)
                 again = dirty[i] == sl.out || (sl.draw_stats && dirty[i] == ctx->draw_stats);
-            if (again) nk = std::max<int64_t>(nk, ctx->h_ring[4 * k] + ctx->h_ring[4 * k + 1]);
+            if (again) nk = std::max<int64_t>(nk, ctx->h_ring[kRingWords * k] + ctx->h_ring[kRingWords * k + 1]);
         }
         if (again) {
             redo[nredo++] = sl;
             need = std::max(need, nk);
             dirty[ndirty++] = sl.out;
             if (sl.draw_stats) dirty[ndirty++] = ctx->draw_stats;
+            newest_redone = newest_redone || k == newest;
         } else {
             accumulate(ctx, k);
         }
         sl.used = false;  // (the re-rendered frames' timings are not accumulated)
+    }
+    // a standing newest frame: rendered again after the others (the same bits into its output,
+    // which nothing later writes), so the context ends on its counts and buffers
+    if (nredo > 0 && newest >= 0 && !newest_redone && newest_sl.spec) {
+        redo[nredo++] = newest_sl;
+        need = std::max<int64_t>(need, newest_sl.fused ? (int64_t)newest_sl.n + ctx->D : ctx->E);
     }
     if (int rc = ensure_entries(ctx, need)) return rc;
     for (int i = 0; i < nredo; ++i)
@@ -541,10 +568,11 @@ int begin_frame(gs_ctx *ctx) {
         const int k = (ctx->cur + 1) % kRing;
         if (!ctx->slot[k].used) {
             ctx->cur = k;
-            // the frame's flag word (k_draw: a prefix miss = 1; k_pre_emit: a look-back that gave
-            // up = 2) starts clear; the kernels only ever store nonzero flags to it.  (The slot's
-            // previous frame is retired, so nothing on the device writes it now.)
-            ctx->h_ring[4 * k + 2] = 0;
+            // the frame's flag words (word 2, k_draw: a prefix miss; word 4, k_pre_emit: a look-back
+            // that gave up) start clear; the kernels only ever store nonzero flags to them.  (The
+            // slot's previous frame is retired, so nothing on the device writes them now.)
+            ctx->h_ring[kRingWords * k + 2] = 0;
+            ctx->h_ring[kRingWords * k + 4] = 0;
             ctx->slot[k] = gs_ctx::Slot{};
             ctx->slot[k].used = true;
             ctx->slot[k].seq = ++ctx->seq;
@@ -596,7 +624,7 @@ int gs_ctx_create(int device, gs_ctx **out) {
         if (hipMemset(ln.bin_counts, 0, gs::kBinCountWords * 4) != hipSuccess)
             return fail(set_error(nullptr, GS_ERR_HIP, "ctx setup failed"));
     }
-    if (hipHostMalloc(&ctx->h_ring, 16 * kRing, hipHostMallocDefault) != hipSuccess ||
+    if (hipHostMalloc(&ctx->h_ring, 4 * kRingWords * kRing, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&ctx->draw_stats, gs::kDrawStatsBytes) != hipSuccess ||
         hipMemset(ctx->draw_stats, 0, gs::kDrawStatsBytes) != hipSuccess)
         return fail(set_error(nullptr, GS_ERR_NOMEM, "ctx allocation failed"));
@@ -1024,6 +1052,7 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
     ctx->L->split = false;
+    ctx->L->sh_partial = defer_sh;
     ctx->L->pe_scene = scene;
     ctx->L->pe_P = P;
     return GS_OK;
@@ -1059,6 +1088,7 @@ int enqueue_pre_emit(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, u
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
     L.split = true;
+    L.sh_partial = false;
     L.keys_sorted = true;
     L.vals_partial = false;
     L.pe_scene = scene;
@@ -1280,7 +1310,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         sl.cap_sel = pd.cap_sel;
         sl.target = ctx->prefix_target;
         sl.turned = pd.use_depth == 0;
-        pd.h_slot = ctx->h_ring_dev + 4 * ctx->cur;
+        pd.h_slot = ctx->h_ring_dev + kRingWords * ctx->cur;
         sl.prefix = true;
         ctx->prefix_frames += 1;
     }
@@ -1316,8 +1346,8 @@ int gs_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint
     // E is needed on the host to size the sort (the reference maps its atomic counter back
     // every frame, src/Splats.cpp:579-583); one 8-byte readback, then emission.
     GS_HIP(ctx, hipStreamSynchronize(ctx->L->stream));  // (V, D) are in the slot's pinned copy
-    ctx->V = ctx->h_ring[4 * ctx->cur];
-    ctx->D = ctx->h_ring[4 * ctx->cur + 1];
+    ctx->V = ctx->h_ring[kRingWords * ctx->cur];
+    ctx->D = ctx->h_ring[kRingWords * ctx->cur + 1];
     ctx->E = ctx->V + ctx->D;
     ctx->e_known = true;
     if (ctx->E >= ((int64_t)1 << 31)) return set_error(ctx, GS_ERR_INVALID, "gs_preprocess: more than 2^31 entries");
@@ -1436,6 +1466,16 @@ int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats) {
     return GS_OK;
 }
 
+int gs_seen_stats(gs_ctx *ctx, gs_frame_stats *stats) {
+    if (!ctx || !stats) return set_error(ctx, GS_ERR_INVALID, "gs_seen_stats: null argument");
+    *stats = gs_frame_stats{};
+    stats->num_splats = ctx->n;
+    stats->visible = ctx->V;
+    stats->duplicates = ctx->D;
+    stats->entries = ctx->E;
+    return GS_OK;
+}
+
 }  // extern "C"
 
 namespace {
@@ -1451,6 +1491,12 @@ int resort_full(gs_ctx *ctx) {
         gs::launch_scan_blocksums(ctx->L->stream, fr, gs::preprocess_blocks(ctx->L->pe_P.n), nullptr, nullptr);
         GS_HIP(ctx, hipGetLastError());
         ctx->L->split = false;
+    }
+    if (ctx->L->sh_partial) {  // the SH colours of every splat with entries: the whole lists are drawn now
+        if (!ctx->L->pe_scene) return set_error(ctx, GS_ERR_STATE, "the frame's scene was destroyed");
+        gs::launch_sh_colour(ctx->L->stream, ctx->L->pe_P, scene_dev(ctx->L->pe_scene), frame_dev(ctx));
+        GS_HIP(ctx, hipGetLastError());
+        ctx->L->sh_partial = false;
     }
     gs::launch_emit(ctx->L->stream, ctx->n, ctx->rec_packed, frame_dev(ctx), ctx->L->keys, ctx->L->vals,
                     (uint32_t)ctx->L->e_cap, nullptr, nullptr);

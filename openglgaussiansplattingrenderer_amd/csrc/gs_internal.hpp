@@ -13,6 +13,8 @@ namespace gs {
 
 // error plumbing: every C entry point returns a status and records a message
 int set_error(gs_ctx *ctx, int code, const std::string &msg);
+// hipSetDevice(ctx's device), the first step of every entry point that allocates or launches
+int ctx_use_device(gs_ctx *ctx);
 
 // host side (gs_host.cpp)
 int ply_count(const char *path, int *n);
@@ -244,6 +246,8 @@ void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEv
 // the splats of ids[0, min(count[0], cap)) -- the kept entries -- and splat 0
 void launch_sh_kept(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const uint32_t *ids,
                     const uint32_t *count, uint32_t cap);
+// GS_FLAG_SH colours of every splat with entries (k_sh_colour; after the frame's emission records)
+void launch_sh_colour(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr);
 bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preprocess) fits this frame
 // prefix_hist != null: also sample the emitted keys into the prefix sort's histogram
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
@@ -256,7 +260,7 @@ struct LookbackDev {
     uint64_t *st_next;     // the other half, cleared by this frame
     uint32_t cap_blocks;
     // polls a workgroup spends waiting on a predecessor before it gives up, emits at the offsets
-    // it has and flags the frame (ring word 2 = 2) for the host to render again; 0 gives up at
+    // it has and flags the frame (ring word 4) for the host to render again; 0 gives up at
     // once (gs_ctx_set_lookback_spin: the test that drives the re-render)
     uint32_t spin_limit;
 };

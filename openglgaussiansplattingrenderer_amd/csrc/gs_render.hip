@@ -861,7 +861,7 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
 // XCD, round-robin over them), so they are running or done; HIP does not promise that order
 // (MI355X_MICROARCH.md, "Workgroup dispatch"), so a wait is bounded: after kLbSpinLimit polls
 // (~tens of ms) it gives up, the workgroup goes on with what it has (every store stays inside the
-// entry capacity) and flags the frame (ring word 2), which the host renders again on the
+// entry capacity) and flags the frame (ring word 4), which the host renders again on the
 // host-synchronous path.  Nothing depends on the order for correctness.  (A ticket counter
 // instead of the workgroup id serialised every workgroup's start on one address: ~33 ns each,
 // 0.2 ms for the 6000 workgroups of C3.)
@@ -965,7 +965,7 @@ __global__ __launch_bounds__(kBlock) void k_pre_emit(PreParams P, SceneDev sc, F
             // (never expected) the frame is rendered again.  Word 2 is cleared by the host when the
             // slot is taken, and nothing on the device writes 0 to it during the frame: a plain
             // store of a nonzero flag (k_draw's prefix miss writes 1) cannot be lost
-            if (fail && fr.h_totals) fr.h_totals[2] = 2u;
+            if (fail && fr.h_totals) fr.h_totals[4] = 1u;
             if (blk == nblocks - 1) {  // the last workgroup: the frame's (V, D)
                 // the device count holds the duplicates emitted (below cap: a frame that did not fit
                 // is detected by the host from the pinned count, and rendered again), so every
@@ -1901,6 +1901,13 @@ void launch_sh_kept(hipStream_t s, const PreParams &P, const SceneDev &sc, const
     else hipLaunchKernelGGL(k_sh_kept<false>, g, dim3(kBlock), 0, s, P, sc, fr, ids, count, cap);
 }
 
+void launch_sh_colour(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr) {
+    if (P.n <= 0) return;
+    const dim3 g((P.n + kBlock - 1) / kBlock);
+    if (P.clean || rec_packed(P)) hipLaunchKernelGGL(k_sh_colour<true>, g, dim3(kBlock), 0, s, P, sc, fr);
+    else hipLaunchKernelGGL(k_sh_colour<false>, g, dim3(kBlock), 0, s, P, sc, fr);
+}
+
 void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, const FrameDev &fr, hipEvent_t start,
                        bool lazy) {
     const int nb = preprocess_blocks(P0.n);
@@ -1924,11 +1931,7 @@ void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, c
         GS_PRE(false, false);
     }
 #undef GS_PRE
-    if (P0.sh) {
-        const dim3 g((P0.n + kBlock - 1) / kBlock);
-        if (P.clean || rec_packed(P)) hipLaunchKernelGGL(k_sh_colour<true>, g, dim3(kBlock), 0, s, P0, sc, fr);
-        else hipLaunchKernelGGL(k_sh_colour<false>, g, dim3(kBlock), 0, s, P0, sc, fr);
-    }
+    if (P0.sh) launch_sh_colour(s, P0, sc, fr);
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {

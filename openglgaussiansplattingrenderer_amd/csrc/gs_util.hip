@@ -24,8 +24,9 @@ __global__ __launch_bounds__(256) void k_stream_copy(const f4v *__restrict__ src
 }  // namespace
 
 extern "C" int gs_stream_copy_gbs(gs_ctx *ctx, size_t bytes, int reps, double *gbs_median, double *gbs_best) {
-    if (!gbs_median || reps < 1 || bytes < 4096) return gs::set_error(ctx, GS_ERR_INVALID, "gs_stream_copy_gbs: bad argument");
     if (!ctx) return gs::set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (!gbs_median || reps < 1 || bytes < 4096) return gs::set_error(ctx, GS_ERR_INVALID, "gs_stream_copy_gbs: bad argument");
+    if (int rc = gs::ctx_use_device(ctx)) return rc;  // the buffers on the ctx's GPU
     if (int rc = gs_sync(ctx)) return rc;  // nothing of the ctx's frames shares the GPU with it
     const size_t n4 = bytes / 16;
     f4v *a = nullptr, *b = nullptr;

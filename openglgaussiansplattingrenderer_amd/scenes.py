@@ -46,3 +46,30 @@ def bicycle_standin_raw(n: int = BICYCLE_N, seed: int = 6131954):
     f_dc = rng.normal(0.0, 0.8, size=(n, 3)).astype(np.float32)
     rot = rng.normal(size=(n, 4)).astype(np.float32)
     return means, f_dc, opacity_logit, log_scale, rot
+
+
+def write_raw_ply(path: str, means3, f_dc3, opacity_logit, log_scale3, rot_raw4, f_rest45=None):
+    """a ply of raw (pre-activation) fields in the tests/plyFileGenerator.py layout (x y z, nx ny nz,
+    f_dc_0..2, f_rest_0..44, opacity, scale_0..2, rot_0..3): what loadSplats reads and activates,
+    so Splats(path, W, H) equals Splats.from_raw(the same fields) bit for bit"""
+    means3 = np.asarray(means3, np.float32).reshape(-1, 3)
+    n = len(means3)
+    hdr = ("ply\nformat binary_little_endian 1.0\nelement vertex %d\n" % n +
+           "".join(f"property float {p}\n" for p in ["x", "y", "z", "nx", "ny", "nz", "f_dc_0", "f_dc_1", "f_dc_2"]) +
+           "".join(f"property float f_rest_{k}\n" for k in range(45)) +
+           "property float opacity\nproperty float scale_0\nproperty float scale_1\nproperty float scale_2\n"
+           "property float rot_0\nproperty float rot_1\nproperty float rot_2\nproperty float rot_3\nend_header\n")
+    with open(path, "wb") as f:
+        f.write(hdr.encode())
+        step = 1 << 20
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            rec = np.zeros((b - a, 62), np.float32)
+            rec[:, 0:3] = means3[a:b]
+            rec[:, 6:9] = np.asarray(f_dc3, np.float32).reshape(-1, 3)[a:b]
+            if f_rest45 is not None:
+                rec[:, 9:54] = np.asarray(f_rest45, np.float32).reshape(-1, 45)[a:b]
+            rec[:, 54] = np.asarray(opacity_logit, np.float32).reshape(-1)[a:b]
+            rec[:, 55:58] = np.asarray(log_scale3, np.float32).reshape(-1, 3)[a:b]
+            rec[:, 58:62] = np.asarray(rot_raw4, np.float32).reshape(-1, 4)[a:b]
+            f.write(rec.tobytes())

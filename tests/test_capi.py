@@ -102,3 +102,17 @@ def test_save_png_roundtrip(tmp_path, flip):
     g.save_png(p, img, flip)
     back = _read_png(p)
     assert np.array_equal(back, img[::-1] if flip else img)
+
+
+def test_raw_ply_loads_as_from_raw(tmp_path):
+    """scenes.write_raw_ply (bench.py's C++ facade scene): the loader's activations of the raw
+    fields equal gs_activate's of the same fields (Splats(path) == Splats.from_raw) bit for bit"""
+    import openglgaussiansplattingrenderer_amd as g
+    from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw, write_raw_ply
+    means, f_dc, logit, log_sc, rot = bicycle_standin_raw(5000, seed=9)
+    p = str(tmp_path / "raw.ply")
+    write_raw_ply(p, means, f_dc, logit, log_sc, rot)
+    m4, cols, op, sc, r4 = g.load_ply(p)
+    cols2, op2, sc2, r42 = g.activate(f_dc, logit, log_sc, rot)
+    assert np.array_equal(m4[:, :3], means) and np.array_equal(cols, cols2) and np.array_equal(op, op2)
+    assert np.array_equal(sc, sc2) and np.array_equal(r4, r42)

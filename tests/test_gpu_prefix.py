@@ -347,3 +347,38 @@ def test_prefix_moving_camera_ignores_stale_depths(motion):
         render_sync(sp, pan(k), ref)
         assert np.array_equal(got[k - 1], ref.download(np.uint8, W * H * 4)), f"pose {k}"
     ctx.close()
+
+
+def test_prefix_miss_keeps_the_newest_frame_readable():
+    """a prefix miss is rendered again after later frames in flight completed.  The
+    context's counts and readbacks must then still be the newest frame's (it is rendered again
+    after the failed one), not the older re-rendered frame's: frame k (a large scene, 256 entries
+    per list: misses), frame k+1 (a small scene, another output), then gs_last_stats and
+    gs_frame_read give frame k+1's counts and values, and both images equal the synchronous ones."""
+    W, H = 1280, 720
+    ctx = g.Context(0)
+    big = g.Splats.from_raw(*bicycle_standin_raw(400_000, seed=3), W, H, ctx=ctx)
+    small = g.Splats.from_raw(*bicycle_standin_raw(3_000, seed=4), W, H, ctx=ctx)
+    u = pose(W, H, 0)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    st_s = render_sync(small, u, ref)
+    img_s = ref.download(np.uint8, W * H * 4)
+    E_s = int(st_s.entries)
+    assert E_s > 0
+    vals_s = small.read(g.GS_READ_VALS, E_s)
+    st_b = render_sync(big, u, ref)  # the newest count seen: the large scene's (prefix-sorted frames next)
+    img_b = ref.download(np.uint8, W * H * 4)
+    assert st_b.entries >= 64 * 256 and st_b.entries != st_s.entries
+    ctx.set_sort_prefix(256)
+    ctx.prefix_stats(reset=True)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(2)]
+    render_spec(big, u, outs[0])
+    render_spec(small, u, outs[1])
+    st = small.stats  # gs_last_stats: syncs, re-renders the miss
+    assert ctx.prefix_stats()["redone"] >= 1
+    assert (st.num_splats, st.visible, st.duplicates, st.entries) == \
+        (st_s.num_splats, st_s.visible, st_s.duplicates, st_s.entries)
+    assert np.array_equal(small.read(g.GS_READ_VALS, E_s), vals_s)
+    assert np.array_equal(outs[0].download(np.uint8, W * H * 4), img_b)
+    assert np.array_equal(outs[1].download(np.uint8, W * H * 4), img_s)
+    ctx.close()

@@ -145,3 +145,52 @@ def test_sh_prefix_sorted_frames_colour_kept_splats(tmp_path, target):
     if target == "whole":
         assert ps["redone"] == 0, ps
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_sh_prefix_frame_then_staged_draw():
+    """a prefix-sorted GS_FLAG_SH frame colours only its kept entries' splats; a staged
+    gs_draw of that frame sorts its lists whole again (resort_full), and must colour every splat
+    with entries first.  The staged draw uses tiles twice the frame's size, so pixels read their
+    lists past the kept prefix (where the colours would be another pose's); it must equal the same
+    staged draw after the host-synchronous frame of that pose."""
+    import ctypes
+    from openglgaussiansplattingrenderer_amd._native import check, lib
+    from openglgaussiansplattingrenderer_amd import _native as N
+    from openglgaussiansplattingrenderer_amd.scenes import bicycle_standin_raw
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    ctx.set_lanes(1)  # one colour buffer: the pose-A colours stay where the B frame does not write
+    sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+    rng = np.random.default_rng(4242)
+    f_dc = ((sp.colours[:, :3] / 255.0 - 0.5) / 0.28209479177387814).astype(np.float32)
+    sp.set_sh(f_dc, rng.normal(0, 0.1, (sp.numSplats, 45)).astype(np.float32))
+    sp.flags = g.GS_FLAG_SH
+    uB = g.main_camera(W, H).uniforms()
+    camA = g.main_camera(W, H)
+    camA.rotateRight(20.0)
+    uA = camA.uniforms()
+    out = g.DeviceBuffer(ctx, W * H * 4)
+    dst = g.DeviceBuffer(ctx, W * H * 4)
+
+    def frame(u, sync):
+        st = N.gs_frame_stats()
+        check(lib().gs_render(ctx.handle, sp._scene, ctypes.byref(u), sp.flags, out.ptr, 1,
+                              ctypes.byref(st) if sync else None), ctx.handle)
+
+    def staged_draw():
+        check(lib().gs_draw(ctx.handle, sp._scene, W, H, ctypes.c_float(W / 8.0), ctypes.c_float(H / 8.0),
+                            g.GS_FLAG_SH, dst.ptr, 1), ctx.handle)
+        return dst.download(np.uint8, W * H * 4)
+
+    frame(uB, True)
+    ref_img = staged_draw()
+    frame(uA, True)  # every splat visible at A now holds A's colour
+    assert ctx.set_sort_prefix() == 32768
+    ctx.prefix_stats(reset=True)
+    frame(uB, False)  # prefix-sorted: B's colours for the kept entries' splats only
+    ctx.sync()
+    ps = ctx.prefix_stats()
+    assert ps["frames"] == 1 and ps["redone"] == 0 and ps["kept"] < ps["entries"] // 2, ps
+    assert np.array_equal(staged_draw(), ref_img)
+    ctx.close()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the committed HEAD's library as lib/libgsplat_hip_old.so beside the working tree's
-# lib/libgsplat_hip.so (for tools/ab_lib.sh on the GPU box).  Run from the repo root, with the
+# lib/libgsplat_hip.so (for `tools/gpu_run.sh ab` on the GPU box).  Run from the repo root, with the
 # change under test uncommitted (with no local changes there is nothing to compare, and a
 # `git stash pop` would restore an unrelated older stash).
 set -e

@@ -60,8 +60,9 @@ print('$2', d['value'], 'fps', d['ms_per_step'], 'ms; serial', fr['serial_ms_per
 profiles)
   # the round's profile collection (TAG, e.g. r04): GPU tests, the kernel trace of the default bench
   # command split by pass, FETCH / WRITE / SQ passes (separate runs), C2 and C5 view 4 traced, the SH
-  # line and the bench line after -> gpurun_out/prof_TAG/ (copy the summaries into profiles/TAG/)
-  TAG=${1:-r04}; R=$(pwd); P=$R/$O/prof_$TAG; mkdir -p $P
+  # line and the bench line after -> gpurun_out/prof_TAG/ (copy the summaries into profiles/TAG/: bench.py reads the newest
+# profiles/rNN/pmc_summary.json and sort_64M_pmc.json)
+  TAG=${1:-r05}; R=$(pwd); P=$R/$O/prof_$TAG; mkdir -p $P
   timeout -k 10 500 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread tests > $O/prof_tests.log 2>&1 || { echo TESTS_FAIL; tail -30 $O/prof_tests.log; exit 1; }
   tail -1 $O/prof_tests.log
   cd /tmp && export TMPDIR=/tmp
@@ -78,7 +79,12 @@ profiles)
       python3 $R/tools/frames.py c3 0 6 > /dev/null 2> $P/sq.err || { echo SQ_FAIL; exit 1; }
   python3 $R/tools/pmc_summary.py $P/fetch/run_counter_collection.csv $P/write/run_counter_collection.csv \
       $P/pmc_summary.json $P/sq/run_counter_collection.csv > $P/pmc_summary.txt
-  cp $P/pmc_summary.json $R/profiles/pmc_summary.json
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $P/sfetch -o run --output-format csv -- \
+      python3 $R/tools/bigsort.py > $P/bigsort_fetch.json 2> $P/sfetch.err || { echo SFETCH_FAIL; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $P/swrite -o run --output-format csv -- \
+      python3 $R/tools/bigsort.py > $P/bigsort_write.json 2> $P/swrite.err || { echo SWRITE_FAIL; exit 1; }
+  python3 $R/tools/sort_pmc_summary.py $P/sfetch/run_counter_collection.csv $P/swrite/run_counter_collection.csv \
+      $P/sort_64M_pmc.json > $P/sort_64M_pmc.txt
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $P/trace_c2 -o run --output-format csv -- \
       python3 $R/bench.py --config c2 --no-cpu-baseline --no-sort-bench > $P/c2_under_trace.json 2> $P/c2.err || { echo C2_FAIL; exit 1; }
   python3 $R/tools/trace_passes.py $P/trace_c2/run_kernel_trace.csv 50 10 100 > $P/c2_trace_by_pass.txt
