@@ -299,8 +299,9 @@ int gs_draw_stats(gs_ctx *ctx, uint64_t out[16], int reset);
  * start, end (s_memrealtime ticks, 100 MHz, low 32 bits), iterations, survivors, (wave,
  * survivor) steps, steps with a needing pixel, (pixel, survivor) needs, list entries in range,
  * survivor steps while <= 64 / <= 128 pixels of the block were active, events while <= 64
- * were, done-mask refreshes (a survivor saturated a pixel), dense-phase survivor steps
- * with > 192 / 129-192 / 65-128 active pixels, dense-phase blend events.
+ * were, done-mask refreshes (a survivor saturated a pixel), dense-phase survivor steps with
+ * events, dense-phase extra event passes (more than 64 events), sparse-phase survivor steps with
+ * events, survivor batches (gathered and culled exactly).
  * Returns the number of blocks copied (<= max_blocks, <= 65536). */
 int gs_draw_block_trace(gs_ctx *ctx, uint32_t *out, int max_blocks);
 int gs_timing_read(gs_ctx *ctx, gs_timing *out);

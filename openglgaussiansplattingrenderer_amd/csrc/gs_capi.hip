@@ -1282,7 +1282,8 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.use_depth = ctx->have_prev_view && turn_cos(ctx->prev_view, u->view) < kPrefixTurnCos ? 0 : 1;
         // (a kept count of the other selection -- with / without the depths -- does not size this one)
         const bool same_sel = ctx->prefix_kept_turned == (pd.use_depth == 0);
-        pd.cap_sel = (uint32_t)(ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
+        // (the class sort holds any kept count: no passes sized from an earlier frame)
+        pd.cap_sel = (uint32_t)(!gs::kPrefixClassSort && ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
                                     ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
                                     : cap_e);
         pd.n = scene->n;

@@ -69,6 +69,15 @@ constexpr int kBinCountWords = 260;  // counts of k_bins_count: [0, 256) tiles, 
 //     that was not sorted (bins[kBinsLimit + t]); a sub-block that reaches it unsaturated flags
 //     the frame (pinned ring word 2 = 1), which is then rendered again with the full sort.
 constexpr int kClasses = 257;
+// the prefix sort's form: 0 (default) -- the kept subset through three more 8-bit LSD passes
+// (13 launches), sized for the previous frame's kept count (cap_sel); 1 -- one pass scatters the
+// kept keys by tile class and one launch sorts each class in LDS (gs_sort.hip k_class_sort, 5
+// launches; bit-exact, but slower at C3 so far: classes over 16k kept keys take a global-memory
+// path)
+#ifndef GS_CLASS_SORT
+#define GS_CLASS_SORT 0
+#endif
+constexpr bool kPrefixClassSort = GS_CLASS_SORT != 0;
 constexpr int kPrefixBuckets = 2048;
 constexpr int kPrefixSample = 128;
 constexpr int kPrefixHistCopies = 2;
@@ -90,8 +99,9 @@ struct PrefixDev {
     // (k_draw's atomicMax; decayed by 1/16 here each frame), or null.  A tile's target is then
     // min(target, 2 * depth + kPrefixDepthSlack): lists the blends read shallowly keep less.
     uint32_t *depth;
-    int32_t use_depth;  // 0: this frame's selection ignores the depths (the camera turned since the
-                        // frame before: they describe another view); its blend still records them
+    int32_t use_depth;  // 0: the camera turned since the frame before (the depths describe another
+                        // view): each class takes its tile neighbourhood's deepest depth
+                        // (GS_PREFIX_TURN_NB); its blend still records them
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };
@@ -99,6 +109,11 @@ struct PrefixDev {
 #define GS_PREFIX_SLACK 4096
 #endif
 constexpr uint32_t kPrefixDepthSlack = GS_PREFIX_SLACK;
+// a turned frame (PrefixDev::use_depth 0) selects each class to twice the deepest depth of its 3 x 3
+// tile neighbourhood plus twice the slack (1), or to the configured target (0)
+#ifndef GS_PREFIX_TURN_NB
+#define GS_PREFIX_TURN_NB 1
+#endif
 constexpr uint32_t kKey1Bits = 0x3f800000u;    // bits(1.0f)
 constexpr uint32_t kKey256Bits = 0x43800000u;  // bits(256.0f)
 // key class: t for the keys in [t, t+1), t < 256; 256 for every other bit pattern
@@ -167,6 +182,8 @@ struct SortScratch {
     size_t hist_cap = 0;           // elements
     uint32_t *row_total = nullptr; // [256], then [16][256] tile counts (zero between sorts)
     uint32_t *bkt = nullptr;       // [2][256]: the bucket form's bucket bases and counts
+    uint32_t *vals_scr = nullptr;  // the prefix class sort's scratch values (long buckets)
+    size_t scr_cap = 0;
 };
 
 // Stable sort of (key, value) pairs: n elements, or -- when dev_count is given -- min(n,
@@ -284,7 +301,7 @@ void launch_ply_activate(hipStream_t s, const float *rec, int count, int base, i
 // (s_memrealtime, 100 MHz), steps, survivors, (wave, survivor) steps, steps with a needing
 // pixel, (pixel, survivor) needs, list entries in range, survivor steps while <= 64 / <= 128
 // pixels were active, events while <= 64 were, done-mask refreshes, dense-phase survivor
-// steps with > 192 / 129-192 / 65-128 active pixels, dense-phase events; the host aggregates
+// steps with events, dense extra event passes, sparse steps with events, survivor batches; the host aggregates
 // (gs_draw_stats)
 constexpr int kDrawTraceBlocks = 65536;
 constexpr int kDrawTraceWords = 16;

@@ -1375,14 +1375,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     }
     unsigned long long st_iter = 0, st_surv = 0, st_kit = 0, st_anyneed = 0, st_pxneed = 0;
     unsigned long long st_kit64 = 0, st_kit128 = 0, st_ev64 = 0, st_refresh = 0;
-    unsigned long long st_a192 = 0, st_a128 = 0, st_a64 = 0, st_dev = 0;  // dense steps by active pixels
-#ifndef GS_STATS_NEV
-#define GS_STATS_NEV 0
-#endif
-#if GS_STATS_NEV
-    uint32_t st_pn = 0;
-    uint64_t st_p0 = 0, st_p1 = 0, st_p2 = 0, st_p3 = 0;
-#endif
+    // the VALU account's counts (tools/valu_account.py): dense steps with events, extra event passes
+    // of dense steps (more than 64 events), sparse steps with events
+    unsigned long long st_a192 = 0, st_a128 = 0, st_a64 = 0;
+    unsigned long long st_batch = 0;  // survivor batches blended (gathered, culled exactly)
     const unsigned long long st_t0 = STATS ? __builtin_amdgcn_s_memrealtime() : 0ull;
     const bool cull = !P.no_cull;
     const int jmax = max(end - 1, 0);
@@ -1598,27 +1594,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 st_ev64 += active <= 64 ? nev : 0;
                 st_anyneed += nev ? 1 : 0;
                 st_pxneed += nev;
-#if GS_STATS_NEV  // (experiment) dense steps by event count, and greedy pairs of consecutive steps
-                  // whose events fit one pass on distinct pixels
-                st_a192 += (nev > 0 && nev <= 16) ? 1 : 0;
-                st_a128 += (nev > 16 && nev <= 32) ? 1 : 0;
-                st_a64 += (nev > 32 && nev <= 48) ? 1 : 0;
-                if (nev) {
-                    const bool merge = st_pn && st_pn + nev <= 64 &&
-                                       !((st_p0 & b0) | (st_p1 & b1) | (st_p2 & b2) | (st_p3 & b3));
-                    st_dev += merge ? 1 : 0;
-                    st_pn = merge ? 0 : nev;
-                    st_p0 = b0;
-                    st_p1 = b1;
-                    st_p2 = b2;
-                    st_p3 = b3;
-                }
-#else
-                st_a192 += active > 192 ? 1 : 0;
-                st_a128 += (active > 128 && active <= 192) ? 1 : 0;
-                st_a64 += (active > 64 && active <= 128) ? 1 : 0;
-                st_dev += nev;
-#endif
+                st_a192 += nev ? 1 : 0;                                   // dense steps with events
+                st_a128 += nev > 64 ? (unsigned long long)((nev - 1) / 64) : 0ull;  // extra event passes
             }
             if (nev != 0) {  // uniform
             // compact this survivor's blend events (slot k's after slots < k, lane order via
@@ -1744,6 +1721,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
                 st_anyneed += nb ? 1 : 0;
                 st_pxneed += __popcll(nb);
                 st_ev64 += __popcll(nb);
+                st_a64 += nb ? 1 : 0;  // sparse steps with events
             }
             if (nb) {  // uniform (no continue: one loop exit)
                 const float o = rl(d.o, src);
@@ -1778,6 +1756,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
 
     // the batch in flight: exact cull and blend (its data arrived; uniform branches)
     auto blend_batch = [&]() __attribute__((always_inline)) {
+        if (STATS) ++st_batch;
         Dd.thr = draw_threshold(Dd.o);
         // A blend that does not take an event adds rgb * 0 (and 0 to w) instead of keeping the
         // state by selects: the same bits when every colour of the batch is finite (the state's
@@ -1880,7 +1859,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             tr[12] = (uint32_t)st_a192;
             tr[13] = (uint32_t)st_a128;
             tr[14] = (uint32_t)st_a64;
-            tr[15] = (uint32_t)st_dev;
+            tr[15] = (uint32_t)st_batch;
         }
     }
 }

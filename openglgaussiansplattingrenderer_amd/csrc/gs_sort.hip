@@ -464,6 +464,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 
         __shared__ __attribute__((aligned(16))) uint32_t s_PG[2 * (kClasses + 1) + 1];
         if (prefix == 1) {
             prefix_counts(tile_counts, pre, cnt, n_max, s_w);
+        } else if (prefix == 3) {  // the class sort's single pass: the class tables, then the draw limits
+            prefix_counts(tile_counts, pre, cnt, n_max, s_w);
+            __syncthreads();  // (workgroup scope: this workgroup's class-table stores before its reads)
+            prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w, s_PG);
         } else if (prefix == 2) {
             prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w, s_PG);
         } else {
@@ -528,8 +532,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 
 //   kPlace   (key, value) in, value out at its position in the full order: the last pass of a
 //            frame's prefix sort (position in the subset + pre.delta[class of the key])
 // PREFIX: the first pass of a prefix sort -- only the keys at or below their class bound move
+// BKT: the digit is the key's bucket (bucket_of: its tile class) -- the scatter of the class sort
 constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2, kPlace = 3;
-template <int W, int FMT, bool PREFIX = false>
+template <int W, int FMT, bool PREFIX = false, bool BKT = false>
 __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
@@ -631,7 +636,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         _Pragma("unroll") for (int k = 0; k < (NI); ++k) {                                            \
             const uint32_t idx = base + k * 64;                                                       \
             const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
-            const uint32_t d = (kk[k] >> shift) & 0xffu;                                              \
+            const uint32_t d = digit_of<BKT>(kk[k], shift);                                           \
             const uint64_t m = match_digit(d, __ballot(valid));                                       \
             rank[k] = count_below(m);                                                                 \
             lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;                          \
@@ -641,7 +646,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
             const uint32_t idx = base + k * 64;                                                       \
             const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
             if (valid && lead[k] == (uint32_t)lane)                                                   \
-                old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[k]);                    \
+                old[k] = atomicAdd(&s_cnt[wid][digit_of<BKT>(kk[k], shift)], old[k]);                 \
         }                                                                                             \
         _Pragma("unroll") for (int k = 0; k < (NI); ++k) rank[k] +=                                   \
             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);                 \
@@ -679,7 +684,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         const uint32_t idx = base + k * 64;
         const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
         if (valid) {
-            const uint32_t d = (kk[k] >> shift) & 0xffu;
+            const uint32_t d = digit_of<BKT>(kk[k], shift);
             const uint32_t pos = s_start[d] + s_cnt[wid][d] + rank[k];
             s_keys[pos] = kk[k];
             if (FMT != kPackIn) s_vals[pos] = vv[k];
@@ -689,7 +694,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     const uint32_t tile_n = PREFIX ? s_tile_n : min((uint32_t)kTile, n - tile0);
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
-        const uint32_t d = (key >> shift) & 0xffu;
+        const uint32_t d = digit_of<BKT>(key, shift);
         const uint32_t o = (uint32_t)(s_gbase[d] + (int32_t)i);
         if (FMT == kPairs) {
             kout[o] = key;
@@ -1071,6 +1076,243 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
         }
 }
 
+// ------------------------------------------------------ the prefix sort's class sort
+// A frame's prefix sort (PrefixDev) keeps, per tile class, the keys at or below the class bound --
+// each class's kept keys a prefix of its sorted list, ~1.2M of C3's 10M entries.  Instead of three
+// more 8-bit LSD passes over the kept subset (9 launches), the first pass scatters the kept keys by
+// their bucket (bucket_of: the tile class; classes 255 and 256 share bucket 255) and one launch
+// sorts every bucket in one workgroup: the bits that vary inside a bucket are few (a tile >= 128's
+// keys 16, [1, 2) 23), so 2-3 LSD passes of 8 bits in LDS order it, and each value goes straight
+// to its position in the full order (position in the kept subset + PrefixDev::delta of its key's
+// class, as kPlace).
+#ifndef GS_CS_WAVES
+#define GS_CS_WAVES 16
+#endif
+constexpr int kCsWaves = GS_CS_WAVES;               // 1024 threads
+constexpr int kCsCap = kCsWaves * 64 * kItems;      // 16384 keys in LDS (128 KB of pairs)
+
+// Stable ranks of one tile of up to W * 64 * IT keys (wave w, item k, lane l = position
+// w*64*IT + k*64 + l; valid below tn) by digit (key >> shift) & 0xff, as rank_tile for W waves:
+// ps[k] = the item's place in the tile's order, s_tdig[d] the tile's count of digit d, s_start[d]
+// its first place.  Waves whose whole range lies past tn rank nothing.  Starts and ends with a
+// barrier.
+template <int W, int IT>
+__device__ __forceinline__ void rank_tile_w(const uint32_t (&kk)[IT], uint32_t tn, int shift, uint32_t (&ps)[IT],
+                                            uint32_t (*s_cnt)[kRadix], uint32_t *s_start, uint32_t *s_wave,
+                                            uint32_t *s_tdig) {
+    static_assert(W * 64 >= kRadix, "one thread per digit");
+    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
+    __syncthreads();  // the previous use of the scratch is done
+    for (int i = threadIdx.x; i < W * kRadix; i += W * 64) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t wbase = wid * (uint32_t)(64 * IT);
+    const uint32_t base = wbase + lane;
+    if (wbase < tn) {  // uniform per wave
+        // items in chunks of CH (the match masks of a chunk, its leaders' returning LDS atomics
+        // back to back, the broadcasts): rank / lead / old for CH items at a time, not all IT
+        constexpr int CH = IT < 4 ? IT : 4;
+#pragma unroll
+        for (int c0 = 0; c0 < IT; c0 += CH) {
+            uint32_t rank[CH], lead[CH], old[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int k = c0 + j;
+                const bool valid = base + k * 64 < tn;
+                const uint64_t m = match_digit((kk[k] >> shift) & 0xffu, __ballot(valid));
+                rank[j] = count_below(m);
+                lead[j] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
+                old[j] = valid ? (uint32_t)__popcll(m) : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int k = c0 + j;
+                const bool valid = base + k * 64 < tn;
+                if (valid && lead[j] == (uint32_t)lane) old[j] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < CH; ++j)
+                ps[c0 + j] = rank[j] + (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[j] << 2), (int)old[j]);
+        }
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (d < kRadix) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t c = s_cnt[w][d];
+            s_cnt[w][d] = tot;
+            tot += c;
+        }
+        s_tdig[d] = tot;
+    }
+    const uint32_t st = block_excl_scan<W>(d < kRadix ? tot : 0u, s_wave);
+    if (d < kRadix) s_start[d] = st;
+    __syncthreads();
+    if (wbase < tn) {
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const uint32_t dg = (kk[k] >> shift) & 0xffu;
+            ps[k] += s_start[dg] + s_cnt[wid][dg];  // (ps held the rank within the wave's digit)
+        }
+    }
+    __syncthreads();
+}
+
+// the 8-bit LSD passes that order a bucket: the bits below the highest one where its smallest and
+// largest key differ (mn, mx: this thread's extremes; W waves)
+template <int W>
+__device__ __forceinline__ int bucket_passes_w(uint32_t mn, uint32_t mx, uint32_t (*s_mm)[W]) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    }
+    if (lane == 0) {
+        s_mm[0][wid] = mn;
+        s_mm[1][wid] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        mn = min(mn, s_mm[0][w]);
+        mx = max(mx, s_mm[1][w]);
+    }
+    const uint32_t diff = mn ^ mx;
+    return diff ? (32 - __builtin_clz(diff) + 7) / 8 : 0;
+}
+
+// One workgroup per bucket b: its kept keys are (kin, vin)[base, base + m) in input order (the
+// first pass's scatter; base = the kept keys of the buckets before it, m = row_total[b]); sorted
+// stably, each value goes to vout[subset position + pre.delta[class of its key]].  Buckets of at
+// most kCsCap keys sort in registers and LDS; longer ones take the same passes through global
+// memory in kCsCap-key tiles, ping-ponging between (kin, vin) and the scratch (ks, vs) over the
+// bucket's range.
+__global__ __launch_bounds__(kCsWaves * 64) void k_class_sort(uint32_t *__restrict__ kin, uint32_t *__restrict__ vin,
+                                                               uint32_t *__restrict__ ks, uint32_t *__restrict__ vs,
+                                                               uint32_t *__restrict__ vout,
+                                                               const uint32_t *__restrict__ row_total, PrefixDev pre) {
+    constexpr int W = kCsWaves, kThreads = W * 64;
+    __shared__ uint32_t s_k[kCsCap], s_v[kCsCap];
+    __shared__ uint32_t s_cnt[W][kRadix];
+    __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
+    __shared__ uint32_t s_wave[W];
+    __shared__ uint32_t s_mm[2][W];
+    __shared__ int32_t s_delta[kClasses];
+    __shared__ uint32_t s_bm[2];
+    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
+    const uint32_t b = blockIdx.x;
+    {  // the bucket's base in the kept subset and its size
+        const uint32_t r = d < kRadix ? row_total[d] : 0u;
+        const uint32_t ex = block_excl_scan<W>(r, s_wave);
+        if (d == (int)b) {
+            s_bm[0] = ex;
+            s_bm[1] = r;
+        }
+        for (int i = threadIdx.x; i < kClasses; i += kThreads) s_delta[i] = pre.delta[i];
+        __syncthreads();
+    }
+    const uint32_t b0 = s_bm[0], m = s_bm[1];
+    if (m == 0) return;  // uniform
+    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems], ps[kItems];
+    auto place = [&](uint32_t pos, uint32_t key, uint32_t val) {
+        vout[(uint32_t)((int32_t)(b0 + pos) + s_delta[key_class(key)])] = val;
+    };
+    if (m <= (uint32_t)kCsCap) {  // uniform: registers and LDS
+        uint32_t mn = 0xffffffffu, mx = 0u;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            const uint32_t pos = base + k * 64;
+            kk[k] = pos < m ? kin[b0 + pos] : 0u;
+            vv[k] = pos < m ? vin[b0 + pos] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if (base + k * 64 < m) {
+                mn = min(mn, kk[k]);
+                mx = max(mx, kk[k]);
+            }
+        const int passes = bucket_passes_w<W>(mn, mx, s_mm);
+        for (int p = 0; p < passes; ++p) {
+            rank_tile_w<W, kItems>(kk, m, 8 * p, ps, s_cnt, s_start, s_wave, s_tdig);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if (base + k * 64 < m) {
+                    s_k[ps[k]] = kk[k];
+                    s_v[ps[k]] = vv[k];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const uint32_t pos = base + k * 64;
+                kk[k] = pos < m ? s_k[pos] : 0u;
+                vv[k] = pos < m ? s_v[pos] : 0u;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if (base + k * 64 < m) place(base + k * 64, kk[k], vv[k]);
+        return;
+    }
+    // long bucket: LSD passes through global memory, kCsCap-key tiles in order
+    int passes;
+    {
+        uint32_t mn = 0xffffffffu, mx = 0u;
+        for (uint32_t i = threadIdx.x; i < m; i += kThreads) {
+            const uint32_t k = kin[b0 + i];
+            mn = min(mn, k);
+            mx = max(mx, k);
+        }
+        passes = bucket_passes_w<W>(mn, mx, s_mm);
+    }
+    uint32_t *sk = kin, *sv = vin, *dk = ks, *dv = vs;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = 8 * p;
+        if (d < kRadix) s_run[d] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += kThreads) atomicAdd(&s_run[(sk[b0 + i] >> shift) & 0xffu], 1u);
+        __syncthreads();
+        {
+            const uint32_t c = d < kRadix ? s_run[d] : 0u;
+            const uint32_t ex = block_excl_scan<W>(c, s_wave);
+            if (d < kRadix) s_run[d] = ex;  // (each thread its own digit)
+        }
+        for (uint32_t t0 = 0; t0 < m; t0 += kCsCap) {
+            const uint32_t tn = min((uint32_t)kCsCap, m - t0);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) {
+                const uint32_t pos = base + k * 64;
+                kk[k] = pos < tn ? sk[b0 + t0 + pos] : 0u;
+                vv[k] = pos < tn ? sv[b0 + t0 + pos] : 0u;
+            }
+            rank_tile_w<W, kItems>(kk, tn, shift, ps, s_cnt, s_start, s_wave, s_tdig);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if (base + k * 64 < tn) {
+                    const uint32_t dg = (kk[k] >> shift) & 0xffu;
+                    const uint32_t o = b0 + s_run[dg] + (ps[k] - s_start[dg]);
+                    dk[o] = kk[k];
+                    dv[o] = vv[k];
+                }
+            __syncthreads();
+            if (d < kRadix) s_run[d] += s_tdig[d];
+        }
+        // the pass's stores before the next pass's loads by the other waves (agent-scope release /
+        // acquire: the acquire invalidates this CU's vector L1, which may hold the range's old lines)
+        __threadfence();
+        __syncthreads();
+        __threadfence();
+        uint32_t *t = sk;
+        sk = dk;
+        dk = t;
+        t = sv;
+        sv = dv;
+        dv = t;
+    }
+    for (uint32_t i = threadIdx.x; i < m; i += kThreads) place(i, sk[b0 + i], sv[b0 + i]);
+}
+
 // The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
 // [8j, 8j + 8) of every copy): walking the sampled histogram from the largest distance (the
 // front of the list) down, the bucket where the count reaches target / kPrefixSample sets
@@ -1082,7 +1324,23 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t c = blockIdx.x, j = threadIdx.x;
     static_assert(kB == 8, "prefix_slot puts bucket 8j + k at word k * (kPrefixBuckets / 8) + j");
     uint32_t v[kB] = {};
-    const uint32_t dep = (pre.depth && pre.use_depth) ? pre.depth[c] : 0u;
+    // a frame whose camera turned since the frame before (use_depth 0): the depths recorded at the
+    // other pose describe content that has moved by a fraction of a tile, so class c takes the
+    // deepest of its 3 x 3 tile neighbourhood (with twice the slack) instead of its own
+    uint32_t dep = 0, slack = kPrefixDepthSlack;
+    if (pre.depth && pre.use_depth) {
+        dep = pre.depth[c];
+    } else if (pre.depth && GS_PREFIX_TURN_NB) {
+        const int tx = (int)(c & 15u), ty = (int)(c >> 4);
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int x = tx + dx, y = ty + dy;
+                if (x >= 0 && x < 16 && y >= 0 && y < 16) dep = max(dep, pre.depth[y * 16 + x]);
+            }
+        slack = 2 * kPrefixDepthSlack;
+    }
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;
@@ -1100,12 +1358,13 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t above = tot - ex - a;  // samples in the buckets of the higher threads
     // the class's target: the configured one, or less where recent blends read the list
     // shallowly (the depth word was read before the scan's barriers; its decay written after)
-    const uint32_t target = dep ? min(pre.target, 2u * dep + kPrefixDepthSlack) : pre.target;
+    const uint32_t target = dep ? min(pre.target, 2u * dep + slack) : pre.target;
     // (decayed by a CAS loop on the current word, not a store of dep - dep / 16: with frames in
     // flight another lane's blend may have raised it since it was read, and a plain store would
     // drop that maximum)
-    if (pre.depth && j == 0 && dep) {
-        uint32_t cur = dep;
+    const uint32_t own = pre.depth ? (pre.use_depth ? dep : pre.depth[c]) : 0u;
+    if (pre.depth && j == 0 && own) {  // (every prefix-sorted frame decays its class's own depth)
+        uint32_t cur = own;
         for (int tries = 0; tries < 16; ++tries) {
             const uint32_t seen = atomicCAS(&pre.depth[c], cur, cur - (cur >> 4));
             if (seen == cur) break;
@@ -1193,6 +1452,7 @@ void sort_free(SortScratch &sc) {
     if (sc.hist) (void)hipFree(sc.hist);
     if (sc.row_total) (void)hipFree(sc.row_total);
     if (sc.bkt) (void)hipFree(sc.bkt);
+    if (sc.vals_scr) (void)hipFree(sc.vals_scr);
     sc = SortScratch{};
 }
 
@@ -1273,6 +1533,43 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     PrefixDev pd = pre ? *pre : PrefixDev{};
     pd.frame_count = dev_count;
+    if (pre && kPrefixClassSort) {
+        // the prefix sort in one scatter pass and one class sort (k_class_sort): 5 launches
+        if (sc.scr_cap < (size_t)n) {
+            if (sc.vals_scr) {
+                (void)hipStreamSynchronize(s);  // in-flight users
+                (void)hipFree(sc.vals_scr);
+            }
+            sc.vals_scr = nullptr;
+            sc.scr_cap = 0;
+            const size_t cap = (size_t)n + (size_t)n / 4 + 4096;
+            if (hipMalloc(&sc.vals_scr, cap * 4) != hipSuccess) {
+                err = "radix sort: out of device memory";
+                return GS_ERR_NOMEM;
+            }
+            sc.scr_cap = cap;
+        }
+        const uint32_t tile = kWaveBig * kWaveTile;
+        const uint32_t nb = (uint32_t)((n + tile - 1) / tile);
+        const uint32_t split = dup_base >= 0 ? (uint32_t)dup_base : kNoSplit;
+        hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
+        hipLaunchKernelGGL((k_upsweep<kWaveBig, true, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, kin,
+                           (uint32_t)n, dev_count, 0, sc.hist, nb, tile_counts, pd, split);
+        auto scan = nb > 4096 ? k_scan_rows<64> : k_scan_rows<4>;
+        hipLaunchKernelGGL(scan, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, nb, (uint32_t)n, dev_count, tile,
+                           sc.row_total, tile_counts, bins, pd, 3);
+        hipLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, kin, vin,
+                           kout, vout, (uint32_t)n, dev_count, 0, sc.hist, nb, sc.row_total, pd, split);
+        // (the kept pairs, by bucket, in the alternate buffers; keys and vals_scr are scratch of long
+        // buckets; the values land in vals)
+        hipExtLaunchKernelGGL(k_class_sort, dim3(kRadix), dim3(kCsWaves * 64), 0, s, nullptr, stop, 0, kout, vout, keys,
+                              sc.vals_scr, vals, sc.row_total, pd);
+        if (hipGetLastError() != hipSuccess) {
+            err = "radix sort: kernel launch failed";
+            return GS_ERR_HIP;
+        }
+        return GS_OK;
+    }
     const int64_t n_sub = pre ? std::min<int64_t>(n, pre->cap_sel) : n;  // passes 1-3 of a prefix sort
     if (pre) {  // the class bounds from the keys the emission sampled
         hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);

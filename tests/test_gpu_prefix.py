@@ -170,13 +170,13 @@ def sheet_and_cluster_scene(u, n_cluster, seed):
     return means, col, op, log_sc, rot
 
 
-def test_prefix_full_fallback_renders_again():
-    """a prefix-sorted frame that keeps more entries than its passes 1-3 were sized for
-    (the previous prefix frame's kept count + 25 % + 64Ki) sorts only part of its kept keys; it is
-    flagged and rendered again with the full sort.  Scene A (an opaque sheet in front of a tight
-    cluster: a few deep lists, every pixel saturating early)
-    keeps ~0.2M entries, then scene B (the C3 stand-in) keeps ~2.2M in the same context: B's
-    first prefix frame takes the `full` path.  Its image equals the host-synchronous frame's."""
+def test_prefix_kept_count_jump():
+    """a prefix-sorted frame that keeps far more entries than the frame before it.  Scene
+    A (an opaque sheet in front of a tight cluster: a few deep lists, every pixel saturating early)
+    keeps ~0.2M entries, then scene B (the C3 stand-in) keeps ~2.2M in the same context.  B's first
+    prefix frame may be rendered again -- its passes 1-3 were sized from A's kept count (the 4-pass
+    form), or it selected with A's per-tile depths -- but at most once, and B's later frames are
+    not; every image equals the host-synchronous frame's."""
     W, H = 1920, 1080
     ctx = g.Context(0)
     ctx.set_lanes(1)  # one lane: the entry buffers B's sync frame grows are the ones B's frame uses
@@ -185,7 +185,7 @@ def test_prefix_full_fallback_renders_again():
     spa = g.Splats.from_raw(*sheet_and_cluster_scene(u, 2_300_000, 8), W, H, ctx=ctx)
     spb = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
     ref = g.DeviceBuffer(ctx, W * H * 4)
-    stb = render_sync(spb, u, ref)  # B's entries sized; the host now knows an entry count
+    render_sync(spb, u, ref)  # B's entries sized; the host now knows an entry count
     img_b = ref.download(np.uint8, W * H * 4)
     sta = render_sync(spa, u, ref)
     img_a = ref.download(np.uint8, W * H * 4)
@@ -199,16 +199,19 @@ def test_prefix_full_fallback_renders_again():
     assert psa["frames"] == 2 and psa["redone"] == 0, psa
     assert np.array_equal(out.download(np.uint8, W * H * 4), img_a)
     kept_a = psa["kept"]
-    render_spec(spb, u, out)  # sized for A's kept count: too small for B's
-    ctx.sync()
-    psb = ctx.prefix_stats()
-    assert psb["frames"] == 1 and psb["redone"] == 1, psb
-    assert psb["kept"] > kept_a * 5 // 4 + 65536, (kept_a, psb)  # the `full` case, not a miss
-    assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
-    # the next B frame is sized from B's kept count: no redo
     render_spec(spb, u, out)
     ctx.sync()
-    assert ctx.prefix_stats()["redone"] == 1
+    psb = ctx.prefix_stats()
+    # (B's first frame selects with the per-tile depths A's blends recorded -- another scene's, far
+    # shallower: it may miss, and is then rendered again; never for its kept count)
+    assert psb["frames"] == 1 and psb["redone"] <= 1, psb
+    assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
+    for _ in range(2):
+        render_spec(spb, u, out)
+    ctx.sync()
+    ps2 = ctx.prefix_stats()
+    assert ps2["frames"] == 3 and ps2["redone"] == psb["redone"], ps2  # B's own depths now
+    assert ps2["kept"] > kept_a * 5 // 4 + 65536, (kept_a, ps2)
     assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
     ctx.close()
 
