@@ -106,8 +106,9 @@ int gs_ctx_set_lanes(gs_ctx *ctx, int lanes);
  * later frame in flight that writes the same output), and the target doubles for the frames after
  * it; after 64 frames in a row without a miss it halves again, never below the configured target.
  * Three misses within 32 prefix-sorted frames turn the prefix sort off for the next 64 frames.
- * A frame whose camera turned more than 0.25 degrees since the frame before keeps every list
- * `target` deep (the depths the blends recorded describe the other view; they still record).
+ * A frame whose camera turned more than 0.25 degrees since the frame before keeps each list twice
+ * as deep as the deepest read of its 3 x 3 tile neighbourhood (plus slack), at most `target`: the
+ * depths the blends recorded describe the other view, whose content moved by part of a tile.
  * target 0: always the full sort.  Frames with fewer than
  * 64 * target (the configured one) entries -- the previous frame's count -- use the full sort.  Setting a target
  * (>= 0) also clears the per-tile depths the blends recorded (a cold start).  Returns the

@@ -1332,14 +1332,15 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
         dep = pre.depth[c];
     } else if (pre.depth && GS_PREFIX_TURN_NB) {
         const int tx = (int)(c & 15u), ty = (int)(c >> 4);
+        constexpr int ry = GS_PREFIX_TURN_NB == 3 ? 0 : 1;  // (3: the row neighbours only)
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
+        for (int dy = -ry; dy <= ry; ++dy)
 #pragma unroll
             for (int dx = -1; dx <= 1; ++dx) {
                 const int x = tx + dx, y = ty + dy;
                 if (x >= 0 && x < 16 && y >= 0 && y < 16) dep = max(dep, pre.depth[y * 16 + x]);
             }
-        slack = 2 * kPrefixDepthSlack;
+        slack = GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack;
     }
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {

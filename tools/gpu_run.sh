@@ -92,7 +92,8 @@ profiles)
       python3 $R/bench.py --view 4 --no-cpu-baseline --no-sort-bench --no-sweep > $P/v4_under_trace.json 2> $P/v4.err || { echo V4_FAIL; exit 1; }
   python3 $R/tools/trace_passes.py $P/trace_v4/run_kernel_trace.csv 50 10 100 > $P/v4_trace_by_pass.txt
   cd $R
-  timeout -k 10 200 python3 bench.py --sh --no-cpu-baseline --no-sort-bench --no-sweep > $P/sh.json 2> $P/sh.err || { echo SH_FAIL; exit 1; }
+  timeout -k 10 200 python3 bench.py --sh --no-cpu-baseline --no-sort-bench --no-sweep --no-facade > $P/sh.json 2> $P/sh.err || { echo SH_FAIL; exit 1; }
+  timeout -k 10 200 python3 tools/valu_account.py c3 > $P/valu_account.txt 2> $P/valu.err || { echo VALU_FAIL; exit 1; }
   timeout -k 10 300 python3 bench.py > $P/bench_latest.json 2> $P/bench.err || { echo BENCH_FAIL; exit 1; }
   echo done ;;
 *) echo "unknown: $what"; exit 2 ;;
