@@ -80,6 +80,8 @@ struct Lane {
     uint2 *cullbox = nullptr;
     int4 *rec = nullptr;
     uint2 *blocksum = nullptr;
+    uint16_t *kdup = nullptr;        // kept emission: per splat its kept duplicates (<= 256)
+    uint2 *blocksum_k = nullptr;     // ... per workgroup its (kept mains, kept duplicates)
     uint32_t *totals = nullptr;      // device [4]
     // entries
     int64_t e_cap = 0;
@@ -209,6 +211,22 @@ struct gs_ctx {
     // rendered again because a wait gave up
     uint32_t lb_spin = gs::kLbSpinLimit;
     uint64_t lb_redo = 0;
+    // the kept emission (gs::KeptDev): a prefix-sorted frame emits only the entries at or below
+    // the class bounds the frame before it selected.  Two bound buffers: frame k reads
+    // theta_buf[theta_cur] (its preprocess counts, its emission writes) and its select writes the
+    // other one for frame k + 1, whose preprocess waits (on the device) for theta_ev, recorded
+    // behind that select.  Each buffer holds two bound sets: [0, kClasses) with the tiles' own
+    // depths, [kClasses, 2 kClasses) with their neighbourhoods' (for a frame k + 1 that turned
+    // since frame k: its content moved by a fraction of a tile).  theta_valid: the read buffer
+    // holds a select's bounds of this scene (else it is reset to "keep every entry", and that
+    // frame sorts all of them).
+    uint32_t *theta_buf[2] = {nullptr, nullptr};
+    int theta_cur = 0;
+    hipEvent_t theta_ev = nullptr;
+    bool theta_valid = false, theta_ev_live = false;
+    bool theta_prev_turned = false;  // the frame before turned (its select's own depths are older)
+    const gs_scene *theta_scene = nullptr;
+    uint64_t kept_frames = 0;
 };
 
 struct gs_scene {
@@ -312,6 +330,7 @@ int ensure_splats(gs_ctx *ctx, int n) {
     int rc;
     if ((rc = grow(ctx, ctx->L->sd, cap)) || (rc = grow(ctx, ctx->L->cullbox, cap)) ||
         (rc = grow(ctx, ctx->L->rec, cap)) || (rc = grow(ctx, ctx->L->blocksum, nb)) ||
+        (rc = grow(ctx, ctx->L->kdup, cap)) || (rc = grow(ctx, ctx->L->blocksum_k, nb)) ||
         (rc = grow(ctx, ctx->L->lb, 2 * (size_t)gs::pre_emit_blocks(cap))))
         return rc;
     // (ordered on the lane's stream with the kernels that use it)
@@ -347,6 +366,8 @@ gs::FrameDev frame_dev(gs_ctx *ctx) {
     f.totals = ctx->L->totals;
     f.h_totals = ctx->h_ring_dev + kRingWords * ctx->cur;
     f.col = ctx->L->col;
+    f.kdup = ctx->L->kdup;
+    f.blocksum_k = ctx->L->blocksum_k;
     return f;
 }
 
@@ -653,7 +674,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
         void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
-                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb};
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb, ln.kdup, ln.blocksum_k};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
@@ -663,6 +684,9 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     }
     if (ctx->draw_stats) (void)hipFree(ctx->draw_stats);
     if (ctx->prefix_depth) (void)hipFree(ctx->prefix_depth);
+    for (uint32_t *t : ctx->theta_buf)
+        if (t) (void)hipFree(t);
+    if (ctx->theta_ev) (void)hipEventDestroy(ctx->theta_ev);
     if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
     for (auto &set : ctx->ev)
         for (auto &e : set)
@@ -1015,6 +1039,12 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 #endif
 constexpr bool kShKept = GS_SH_KEPT != 0;
 
+// prefix-sorted frames of large scenes emit only their kept entries (the bounds of the frame before)
+#ifndef GS_KEPT_EMIT
+#define GS_KEPT_EMIT 1
+#endif
+constexpr bool kKeptEmission = GS_KEPT_EMIT != 0;
+
 #ifndef GS_QUEUE_FRAC
 #define GS_QUEUE_FRAC 2  // the queued preprocess when fewer than n / GS_QUEUE_FRAC splats were visible
 #endif
@@ -1024,7 +1054,7 @@ bool lazy_loads(const gs_ctx *ctx, int n) { return ctx->n == n && ctx->e_known &
 // defer_sh (a prefix-sorted GS_FLAG_SH frame): no SH colours here -- k_sh_kept colours the kept
 // entries' splats after the sort (enqueue_sh_kept)
 int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t flags,
-                       bool defer_sh = false) {
+                       bool defer_sh = false, const uint32_t *theta_in = nullptr) {
     const int n = scene->n;
     const bool sh = (flags & GS_FLAG_SH) != 0;
     if (sh && !scene->sh) return set_error(ctx, GS_ERR_INVALID, "GS_FLAG_SH: the scene has no SH (gs_scene_set_sh)");
@@ -1042,12 +1072,13 @@ int enqueue_preprocess(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u,
     for (int c = 0; c < 3; ++c)
         P.campos[c] = -(u->view[4 * c + 0] * u->view[12] + u->view[4 * c + 1] * u->view[13] +
                         u->view[4 * c + 2] * u->view[14]);
-    const gs::FrameDev fr = frame_dev(ctx);
+    gs::FrameDev fr = frame_dev(ctx);
+    fr.theta_in = theta_in;  // (kept emission: the bounds this frame's preprocess counts with)
     const int nb = gs::preprocess_blocks(n);
     // k_scan_blocksums writes (V, D) to ctx->L->totals and to this slot's pinned host copy
     gs::PreParams Pl = P;
     if (defer_sh) Pl.sh = 0;
-    gs::launch_preprocess(ctx->L->stream, Pl, scene_dev(scene), fr, fev(ctx, 0), lazy_loads(ctx, n));
+    gs::launch_preprocess(ctx->L->stream, Pl, scene_dev(scene), fr, fev(ctx, 0), !theta_in && lazy_loads(ctx, n));
     gs::launch_scan_blocksums(ctx->L->stream, fr, nb, nb > 0 ? nullptr : fev(ctx, 0), fev(ctx, 1));
     GS_HIP(ctx, hipGetLastError());
     ctx->n = n;
@@ -1112,12 +1143,13 @@ int enqueue_emit(gs_ctx *ctx, uint32_t *prefix_hist = nullptr) {
 // only) when the splat ids fit 24 bits; gs_frame_read(GS_READ_KEYS) then sorts again.
 // small: the small-frame form (with bins, no prefix; keys come out sorted)
 int enqueue_sort(gs_ctx *ctx, int64_t E, const uint32_t *count, bool with_bins = false,
-                 const gs::PrefixDev *pre = nullptr, int64_t dup_base = -1, bool small = false) {
+                 const gs::PrefixDev *pre = nullptr, int64_t dup_base = -1, bool small = false,
+                 const gs::KeptSort *kept = nullptr) {
     small = small && with_bins && !pre;
     const bool keys_out = small || (!pre && (!with_bins || ctx->n > (1 << 24)));
     if (int rc = gs::sort_pairs(ctx->L->stream, ctx->L->sort, ctx->L->keys, ctx->L->vals, E, ctx->err, count, fev(ctx, 4),
                                 fev(ctx, 5), with_bins ? ctx->L->bins : nullptr, keys_out, pre, dup_base, small,
-                                small && ctx->bucket_sort))
+                                small && ctx->bucket_sort, kept))
         return set_error(ctx, rc, ctx->err);
     ctx->L->keys_sorted = keys_out;
     ctx->L->vals_partial = pre != nullptr;
@@ -1251,6 +1283,21 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         prefix = false;
     }
     gs::PrefixDev pd{};
+    // passes 1-3 sized for the kept count of the newest retired prefix-sorted frame of the same
+    // selection (with / without the depths) + 25 % (+ 64Ki); else every entry.  (Scaled by the
+    // depth since: a miss doubles it, and the kept count roughly with it; the class sort holds any
+    // kept count: no passes sized from an earlier frame.)
+    auto cap_for = [&](bool turned_sel) -> uint32_t {
+        const int64_t cap_e = ctx->L->e_cap;
+        const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
+                                 ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
+                                 : (int64_t)ctx->prefix_kept;
+        const bool same_sel = ctx->prefix_kept_turned == turned_sel;
+        return (uint32_t)(!gs::kPrefixClassSort && ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
+                              ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
+                              : cap_e);
+    };
+    bool sel_turned = false;  // the selection this frame keeps by: the turned (neighbourhood) form
     if (prefix) {
         if (!ctx->L->pre_buf) {
             GS_HIP(ctx, hipMalloc(&ctx->L->pre_buf, gs::kPrefixWords * 4));
@@ -1263,13 +1310,6 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.nsel = pd.counts + (size_t)gs::kPrefixCopies * (gs::kClasses + 1);
         pd.delta = (int32_t *)(pd.nsel + 2);
         pd.cls = (uint32_t *)(pd.delta + gs::kClasses);
-        // passes 1-3 sized for the kept count of the newest retired prefix-sorted frame + 25 %
-        // (+ 64Ki); the first one: every entry
-        const int64_t cap_e = ctx->L->e_cap;
-        // (scaled by the depth since: a miss doubles it, and the kept count roughly with it)
-        const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
-                                 ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
-                                 : (int64_t)ctx->prefix_kept;
         pd.target = (uint32_t)ctx->prefix_target;
         if (!ctx->prefix_depth) {  // (zeroed before any frame can read it)
             GS_HIP(ctx, hipMalloc(&ctx->prefix_depth, 256 * 4));
@@ -1280,22 +1320,62 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         // depths describe another view (their tiles' contents moved), so this frame's lists are
         // kept to the configured target instead (a fast pan missed on nearly every frame)
         pd.use_depth = ctx->have_prev_view && turn_cos(ctx->prev_view, u->view) < kPrefixTurnCos ? 0 : 1;
-        // (a kept count of the other selection -- with / without the depths -- does not size this one)
-        const bool same_sel = ctx->prefix_kept_turned == (pd.use_depth == 0);
-        // (the class sort holds any kept count: no passes sized from an earlier frame)
-        pd.cap_sel = (uint32_t)(!gs::kPrefixClassSort && ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
-                                    ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
-                                    : cap_e);
+        sel_turned = pd.use_depth == 0;
+        pd.cap_sel = cap_for(sel_turned);
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
     }
     const bool fused = gs::preprocess_blocks(scene->n) <= kFusedMaxBlocks;
     // GS_FLAG_SH with the prefix sort: colour only the kept entries' splats, after the sort
     const bool defer_sh = prefix && !fused && (flags & GS_FLAG_SH) && kShKept;
+    // the kept emission (gs::KeptDev): a prefix-sorted frame of a large scene, not mostly culled,
+    // emits only the entries at or below the bounds the frame before it selected
+    const bool kept_mode = prefix && !fused && kKeptEmission && !lazy_loads(ctx, scene->n);
+    const uint32_t *theta_in = nullptr;
+    if (kept_mode) {
+        for (uint32_t *&t : ctx->theta_buf)
+            if (!t) GS_HIP(ctx, hipMalloc(&t, 2 * gs::kClasses * 4));
+        if (!ctx->theta_ev) GS_HIP(ctx, hipEventCreateWithFlags(&ctx->theta_ev, hipEventDisableTiming));
+        const bool keep_all = !ctx->theta_valid || ctx->theta_scene != scene;
+        if (keep_all) {  // no bounds of this scene yet: keep everything
+            static std::vector<uint32_t> all = [] {
+                std::vector<uint32_t> a(2 * gs::kClasses);
+                for (int c = 0; c < 256; ++c) a[c] = a[gs::kClasses + c] = gs::class_hi((uint32_t)c) - 1u;
+                a[256] = a[gs::kClasses + 256] = 0xffffffffu;
+                return a;
+            }();
+            if (ctx->theta_ev_live) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
+            GS_HIP(ctx, hipMemcpyAsync(ctx->theta_buf[ctx->theta_cur], all.data(), 2 * gs::kClasses * 4,
+                                       hipMemcpyHostToDevice, ctx->L->stream));
+            // another scene's per-tile depths would size the bounds this frame selects for the
+            // next one (which, unlike this frame, cannot hold more): forget them, as a new
+            // context starts
+            if (ctx->theta_scene && ctx->theta_scene != scene && ctx->prefix_depth)
+                GS_HIP(ctx, hipMemsetAsync(ctx->prefix_depth, 0, 256 * 4, ctx->L->stream));
+            ctx->theta_valid = true;
+            ctx->theta_scene = scene;
+        } else if (ctx->theta_ev_live) {  // the select that wrote them (the frame before, another lane)
+            GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
+        }
+        // the neighbourhood bounds when this frame turned since the frame before, or that frame
+        // did (its select read depths of the pose before it)
+        const bool turned = pd.use_depth == 0;
+        sel_turned = turned || ctx->theta_prev_turned;
+        theta_in = ctx->theta_buf[ctx->theta_cur] + (sel_turned ? gs::kClasses : 0);
+        ctx->theta_prev_turned = turned;
+        // this frame's select: the next frame's bounds, both forms
+        pd.theta = ctx->theta_buf[ctx->theta_cur ^ 1];
+        pd.theta_turn = pd.theta + gs::kClasses;
+        pd.use_depth = 1;
+        // the sort's four passes sized as passes 1-3 are (a frame keeping every entry: all of them)
+        pd.cap_sel = keep_all ? (uint32_t)ctx->L->e_cap : cap_for(sel_turned);
+    } else {
+        ctx->theta_valid = false;  // (a frame between them: the bounds would be stale)
+    }
     if (fused) {
         if (int rc = enqueue_pre_emit(ctx, scene, u, flags, prefix ? pd.hist : nullptr)) return rc;
     } else {
-        if (int rc = enqueue_preprocess(ctx, scene, u, flags, defer_sh)) return rc;
+        if (int rc = enqueue_preprocess(ctx, scene, u, flags, defer_sh, theta_in)) return rc;
     }
     gs_ctx::Slot &sl = ctx->slot[ctx->cur];
     sl.spec = true;
@@ -1310,7 +1390,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     if (prefix) {
         sl.cap_sel = pd.cap_sel;
         sl.target = ctx->prefix_target;
-        sl.turned = pd.use_depth == 0;
+        sl.turned = sel_turned;
         pd.h_slot = ctx->h_ring_dev + kRingWords * ctx->cur;
         sl.prefix = true;
         ctx->prefix_frames += 1;
@@ -1318,10 +1398,29 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     int rc;
     // the emission (the fused kernel's is done); the sort sized by the capacity (the entry count
     // stays on the device), reading the fused kernel's split layout as V + D entries
-    if (!fused && (rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr))) return rc;
-    if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
-                           ctx->E < ctx->small_sort_entries)))
+    gs::KeptSort ks{ctx->L->totals + 2, ctx->theta_ev};
+    if (kept_mode) {
+        gs::FrameDev fr = frame_dev(ctx);
+        fr.theta_in = theta_in;
+        // (the sort scratch holds the tile counters the emission adds to)
+        if (int rc2 = gs::sort_ensure(ctx->L->sort, ctx->L->e_cap, ctx->err, ctx->L->stream)) return set_error(ctx, rc2, ctx->err);
+        gs::KeptDev kd{ctx->L->sort.row_total + 256, pd.counts, pd.hist};
+        ctx->L->keys_sorted = true;
+        ctx->L->vals_partial = false;
+        gs::launch_emit_kept(ctx->L->stream, ctx->n, ctx->rec_packed, fr, ctx->L->keys, ctx->L->vals, (uint32_t)ctx->L->e_cap,
+                             kd, fev(ctx, 2), fev(ctx, 3));
+        GS_HIP(ctx, hipGetLastError());
+        ctx->kept_frames += 1;
+    } else if (!fused && (rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr))) {
         return rc;
+    }
+    if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
+                           ctx->E < ctx->small_sort_entries, kept_mode ? &ks : nullptr)))
+        return rc;
+    if (kept_mode) {  // the next kept frame reads the bounds this frame's select writes
+        ctx->theta_cur ^= 1;
+        ctx->theta_ev_live = true;
+    }
     if (defer_sh) {  // the kept entries' values: the sort's pass-2 output, left in the alternate buffer
         gs::launch_sh_kept(ctx->L->stream, ctx->L->pe_P, scene_dev(scene), frame_dev(ctx), ctx->L->sort.vals_alt,
                            pd.nsel, pd.cap_sel);
@@ -1438,6 +1537,7 @@ int render_impl(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     };
     if (!stats && out_on_device && ctx->e_known && !(flags & GS_FLAG_TIMING))
         return seen(render_spec(ctx, scene, u, flags, out_rgba8));
+    ctx->theta_valid = false;  // (a kept emission after it starts from every entry)
     if (int rc = seen(render_sync(ctx, scene, u, flags, out_rgba8, out_on_device, stats))) return rc;
     if (flags & GS_FLAG_TIMING) {
         hipEvent_t *e = ctx->ev[ctx->cur];
@@ -1521,6 +1621,7 @@ int gs_ctx_set_sort_prefix(gs_ctx *ctx, int target, int *current) {
         ctx->prefix_miss_at[0] = ctx->prefix_miss_at[1] = ~0ull;
         ctx->prefix_after_miss = false;
         ctx->prefix_kept = 0;  // (passes 1-3 of the next prefix-sorted frame sized for every entry)
+        ctx->theta_valid = false;  // (the next kept emission starts from every entry)
         if (ctx->prefix_depth) {  // a new target starts from a cold per-tile depth table (after the
             // frames in flight, whose blends write it)
             if (int rc = use_device(ctx)) return rc;

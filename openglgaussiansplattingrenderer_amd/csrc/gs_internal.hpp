@@ -93,6 +93,7 @@ struct PrefixDev {
     uint32_t *cls;     // [kClasses + 1] class starts in the full order (then E), [kClasses] ends of their kept keys
     uint32_t cap_sel;  // elements passes 1-3 are sized for (more kept: the host renders the frame again)
     const uint32_t *frame_count;  // the frame's device (V, D) (set by sort_pairs)
+    uint32_t cap_all;             // the entry capacity, the bound of V + D (set by sort_pairs)
     uint32_t *h_slot;  // mapped pinned ring slot of the frame: [3] = kept keys (diagnostics), or null
     uint32_t target;   // entries per class to keep at least
     // [256] per tile: the deepest window position any recent blend of the context reached
@@ -102,6 +103,9 @@ struct PrefixDev {
     int32_t use_depth;  // 0: the camera turned since the frame before (the depths describe another
                         // view): each class takes its tile neighbourhood's deepest depth
                         // (GS_PREFIX_TURN_NB); its blend still records them
+    // a kept emission's select (theta: the next frame's bounds, with the own depths): the bounds
+    // for a next frame that turned (the neighbourhood form) here [kClasses], else null
+    uint32_t *theta_turn;
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };
@@ -199,10 +203,17 @@ struct SortScratch {
 // dup_base >= 0 (with dev_count): the input is k_pre_emit's split layout, V = dev_count[0] mains
 // at [0, V) and the dev_count[1] duplicates at [dup_base, dup_base + D); the first pass reads it
 // as one array of V + D entries (n is then the capacity of that virtual array).
+// kept != null (with pre): the input is a kept emission (k_emit_kept): kept->count[0] + [1] entries,
+// already filtered by the class bounds and counted (tile counts, kept per class); the select
+// writes the NEXT frame's bounds (pre->theta) and kept->after_select is recorded behind it
+struct KeptSort {
+    const uint32_t *count;
+    hipEvent_t after_select;
+};
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count = nullptr, hipEvent_t start = nullptr, hipEvent_t stop = nullptr,
                uint32_t *bins = nullptr, bool keys_out = true, const PrefixDev *pre = nullptr,
-               int64_t dup_base = -1, bool small = false, bool bucket = false);
+               int64_t dup_base = -1, bool small = false, bool bucket = false, const KeptSort *kept = nullptr);
 // small (not with pre): the form for few entries -- 8 launches instead of 12 (k_sweep_small);
 // keys and values come out sorted.  Any n is sorted correctly; it pays off while n is small.
 // bucket (with small): 3 launches -- a stable scatter by tile (bucket_of) and k_bucket_sort's
@@ -247,9 +258,27 @@ struct FrameDev {
     uint2 *cullbox;    // conservative pixel box of the alpha >= 1/255 region (int16 bounds, pack_box)
     int4 *rec;         // emission records: 8-byte packed (rec_packed) or (z01 bits, tileX, tileY (-1: no entries), rect)
     uint2 *blocksum;   // per-workgroup (main, dup) sums -> exclusive offsets
-    uint32_t *totals;  // [0]=V [1]=D
+    uint32_t *totals;  // [0]=V [1]=D; kept emission: [2] kept mains, [3] kept duplicates
     uint32_t *h_totals;  // mapped pinned host copy of (V, D) for this frame, or null
     float4 *col;         // per-frame colours of GS_FLAG_SH frames (else null)
+    // kept emission (a prefix-sorted frame with the class bounds of an earlier frame's select,
+    // see KeptDev): the bounds this frame uses, per splat its kept duplicates, per workgroup
+    // the (kept mains, kept duplicates) sums -> exclusive offsets
+    const uint32_t *theta_in = nullptr;  // [kClasses], or null (kept emission off)
+    uint16_t *kdup = nullptr;  // (up to 256: a 16 x 16 rect without the main tile)
+    uint2 *blocksum_k = nullptr;
+};
+// The kept emission's counters (k_emit_kept): it emits only the entries at or below their class
+// bound (PrefixDev::theta of the frame before: every class's kept keys a prefix of its sorted
+// list, as in the first pass of the prefix sort), and counts what that pass's upsweep counted
+// over every entry -- the tile counts of the bins, the keys above 1e6, the kept keys per class
+// and the keys below 1.0 -- and samples the keys for this frame's select (the next frame's
+// bounds).
+constexpr int kTileCopyCount = 16;  // copies of the frame's tile counters (gs_sort.hip kTileCopies)
+struct KeptDev {
+    uint32_t *tile_counts;  // [kTileCopies = 16][256] tile counts, then [16] keys above 1e6 (SortScratch::row_total + 256)
+    uint32_t *counts;       // PrefixDev::counts: [kPrefixCopies][kClasses] kept per class, then [kPrefixCopies] keys < 1.0
+    uint32_t *phist;        // PrefixDev::hist (sampled distances to the class bounds)
 };
 int preprocess_blocks(int n);  // workgroups of k_preprocess / k_emit (= block sums)
 int pre_emit_blocks(int n);    // workgroups of k_pre_emit (= its look-back status words)
@@ -269,6 +298,9 @@ bool rec_packed(const PreParams &P);  // the 8-byte emission record (k_preproces
 // prefix_hist != null: also sample the emitted keys into the prefix sort's histogram
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
                  hipEvent_t start, hipEvent_t stop, uint32_t *prefix_hist = nullptr);
+// the kept emission (k_emit_kept; fr.theta_in set, after a KEPT preprocess and block-sum scan)
+void launch_emit_kept(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+                      const KeptDev &kd, hipEvent_t start, hipEvent_t stop);
 // The fused preprocess + emission of a frame enqueued without a host round trip (k_pre_emit):
 // its decoupled look-back state, two halves per frame lane used by alternate frames (each frame
 // clears the other half for the next one).

@@ -109,6 +109,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 // exclusive block scan over 256 threads; returns prefix, *total = block sum
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *s_wave, uint32_t *total) {
     const int lane = lane_id(), wid = threadIdx.x >> 6;
@@ -464,16 +470,45 @@ __device__ __forceinline__ uint32_t rec_dups(const int4 &rc) {
     return rc.y >= 0 ? (uint32_t)(rectCount - mainInRect) : 0u;
 }
 
-template <bool PACK, bool CLEAN, bool LAZY>
+// The kept emission's count for one splat's entries (emission record rc, with entries): whether
+// its main entry and how many of its duplicates have keys at or below their class bound -- the
+// same keys k_emit_kept computes (tile + z01 as floats), the same test
+__device__ __forceinline__ uint2 kept_of(const int4 &rc, const uint32_t *s_theta) {
+    const float z = u2f((uint32_t)rc.x);
+    const uint32_t mkey = f2u((float)((uint32_t)rc.z * 16u + (uint32_t)rc.y) + z);
+    const uint32_t km = mkey <= s_theta[key_class(mkey)] ? 1u : 0u;
+    const int minX = rc.w & 0xff, maxX = (rc.w >> 8) & 0xff, minY = (rc.w >> 16) & 0xff, maxY = (rc.w >> 24) & 0xff;
+    uint32_t kd = 0;
+    for (int ty = minY; ty <= maxY; ++ty)
+        for (int tx = minX; tx <= maxX; ++tx) {
+            if (tx == rc.y && ty == rc.z) continue;  // the main tile (preprocess.glsl:171-188)
+            const uint32_t key = f2u((float)(ty * 16 + tx) + z);
+            kd += key <= s_theta[key_class(key)] ? 1u : 0u;
+        }
+    return make_uint2(km, kd);
+}
+
+template <bool PACK, bool CLEAN, bool LAZY, bool KEPT = false>
 __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc, FrameDev fr) {
     __shared__ uint32_t s_wave[kBlock / 64];
-    uint32_t n_main = 0, n_dup = 0;
+    __shared__ uint32_t s_theta[KEPT ? kClasses : 1];
+    if (KEPT) {
+        for (int c = threadIdx.x; c < kClasses; c += kBlock) s_theta[c] = fr.theta_in[c];
+        __syncthreads();
+    }
+    uint32_t n_main = 0, n_dup = 0, n_km = 0, n_kd = 0;
 #pragma unroll 1
     for (int it = 0; it < kPer; ++it) {
         const int i = blockIdx.x * kSplatsPerBlock + it * kBlock + threadIdx.x;
         const int4 rc = preprocess_one<CLEAN, LAZY>(P, sc, fr, i, i < P.n);
         n_main += rc.y >= 0 ? 1u : 0u;
         n_dup += rec_dups(rc);
+        if (KEPT && rc.y >= 0) {  // (only splats with entries: i < P.n)
+            const uint2 k = kept_of(rc, s_theta);
+            n_km += k.x;
+            n_kd += k.y;
+            fr.kdup[i] = (uint16_t)k.y;
+        }
         if (i < P.n) {
             if (PACK)
                 reinterpret_cast<uint2 *>(fr.rec)[i] =
@@ -492,6 +527,11 @@ __global__ __launch_bounds__(kBlock) void k_preprocess(PreParams P, SceneDev sc,
         tot_dup = tot >> 11;
     }
     if (threadIdx.x == 0) fr.blocksum[blockIdx.x] = make_uint2(tot_main, tot_dup);
+    if (KEPT) {  // the kept entries' block sums (the same packing)
+        uint32_t tot;
+        block_excl_scan256(n_km | (n_kd << 11), s_wave, &tot);
+        if (threadIdx.x == 0) fr.blocksum_k[blockIdx.x] = make_uint2(tot & 0x7ffu, tot >> 11);
+    }
 }
 
 // The same records with the NDC cull compacted out (QUEUE form).  kQWaves waves share a
@@ -614,10 +654,9 @@ __global__ __launch_bounds__(64 * kQWaves) void k_preprocess_q(PreParams P, Scen
 // drain); each thread owns 24 consecutive sums per round (independent loads issued together):
 // one round covers 6144 block sums = 6.3M splats.
 constexpr int kScanThreads = 256, kScanPer = 24;
-__global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, int nblocks) {
+// one array of (a, b) block sums -> exclusive offsets; returns the totals (thread 0)
+__device__ __forceinline__ uint2 scan_pairs(uint2 *bs, int nblocks, uint32_t *s_w0, uint32_t *s_w1, uint32_t *s_carry) {
     constexpr int W = kScanThreads / 64;
-    __shared__ uint32_t s_w0[W], s_w1[W];
-    __shared__ uint32_t s_carry[2];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) s_carry[0] = s_carry[1] = 0;
     __syncthreads();
@@ -625,7 +664,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, in
         const int i0 = base + threadIdx.x * kScanPer;
         uint2 v[kScanPer];
 #pragma unroll
-        for (int k = 0; k < kScanPer; ++k) v[k] = (i0 + k < nblocks) ? fr.blocksum[i0 + k] : make_uint2(0, 0);
+        for (int k = 0; k < kScanPer; ++k) v[k] = (i0 + k < nblocks) ? bs[i0 + k] : make_uint2(0, 0);
         uint32_t a0 = 0, a1 = 0;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
@@ -650,7 +689,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, in
         o1 += c1 - a1;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
-            if (i0 + k < nblocks) fr.blocksum[i0 + k] = make_uint2(o0, o1);
+            if (i0 + k < nblocks) bs[i0 + k] = make_uint2(o0, o1);
             o0 += v[k].x;
             o1 += v[k].y;
         }
@@ -661,12 +700,33 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, in
         }
         __syncthreads();
     }
+    return make_uint2(s_carry[0], s_carry[1]);
+}
+
+// exclusive scan of the per-block (main, dup) sums; totals -> fr.totals[0..1] (KEPT: also the
+// kept entries' sums, totals -> fr.totals[2..3]).
+// One workgroup of 256 (a small workgroup finds room on a CU beside the previous frame's blend,
+// which occupies most wave slots while this runs; 1024 threads waited ~50 us for one CU to
+// drain); each thread owns 24 consecutive sums per round (independent loads issued together):
+// one round covers 6144 block sums = 6.3M splats.
+template <bool KEPT = false>
+__global__ __launch_bounds__(kScanThreads) void k_scan_blocksums(FrameDev fr, int nblocks) {
+    constexpr int W = kScanThreads / 64;
+    __shared__ uint32_t s_w0[W], s_w1[W];
+    __shared__ uint32_t s_carry[2];
+    const uint2 t = scan_pairs(fr.blocksum, nblocks, s_w0, s_w1, s_carry);
+    uint2 tk = make_uint2(0, 0);
+    if (KEPT) tk = scan_pairs(fr.blocksum_k, nblocks, s_w0, s_w1, s_carry);
     if (threadIdx.x == 0) {
-        fr.totals[0] = s_carry[0];
-        fr.totals[1] = s_carry[1];
+        fr.totals[0] = t.x;
+        fr.totals[1] = t.y;
+        if (KEPT) {
+            fr.totals[2] = tk.x;
+            fr.totals[3] = tk.y;
+        }
         if (fr.h_totals) {  // mapped pinned host memory: the host reads it after the frame's event
-            fr.h_totals[0] = s_carry[0];
-            fr.h_totals[1] = s_carry[1];
+            fr.h_totals[0] = t.x;
+            fr.h_totals[1] = t.y;
             fr.h_totals[3] = 0;
         }
     }
@@ -843,6 +903,196 @@ __global__ __launch_bounds__(kBlock) void k_emit(int n, FrameDev fr, uint32_t *_
     }
 }
 
+// The kept emission of a prefix-sorted frame (KeptDev): k_emit's walk over every entry, in the
+// same order and with the same keys, but only the entries at or below their class bound (the
+// bounds an earlier frame's select chose, fr.theta_in) are written -- compacted, kept mains at
+// [0, KV) in splat order, kept duplicates at [KV, KV + KD) splat-major (k_preprocess counted
+// them: fr.kdup, fr.blocksum_k scanned), i.e. the emission order restricted to them, which a
+// stable sort turns into the full sort restricted to them.  Over every entry it counts what the
+// prefix sort's first pass counted (the tile counts, the keys above 1e6, the kept keys per
+// class, the keys below 1.0) and samples one entry in kPrefixSample by full position for this
+// frame's select.  The sort then runs its four passes over the kept entries alone.
+template <bool PACK>
+__global__ __launch_bounds__(kBlock) void k_emit_kept(int n, FrameDev fr, uint32_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ vals, uint32_t cap, KeptDev kd) {
+    constexpr int kR = 4;  // counter replicas (lane % 4)
+    __shared__ uint16_t s_incl[kBlock / 64][64];
+    __shared__ uint32_t s_theta[kClasses];
+    __shared__ uint32_t s_tiles[256 * kR];
+    __shared__ uint32_t s_kept[kClasses * kR];
+    __shared__ uint32_t s_above, s_low;
+    __shared__ uint4 s_tot[kBlock / 64];
+    for (int c = threadIdx.x; c < kClasses; c += kBlock) s_theta[c] = fr.theta_in[c];
+    for (int c = threadIdx.x; c < 256 * kR; c += kBlock) s_tiles[c] = 0;
+    for (int c = threadIdx.x; c < kClasses * kR; c += kBlock) s_kept[c] = 0;
+    if (threadIdx.x == 0) s_above = s_low = 0;
+    const uint2 off = fr.blocksum[blockIdx.x], koff = fr.blocksum_k[blockIdx.x];
+    const uint32_t V = fr.totals[0], KV = fr.totals[2];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t rep = (uint32_t)lane & (kR - 1);
+    const int wbase = blockIdx.x * kSplatsPerBlock + wid * (kPer * 64);
+    uint2 raws[kPer];
+    int4 rcs[kPer];
+    uint32_t incl_d[kPer];
+    uint64_t hasm[kPer];
+    uint32_t tot_m = 0, tot_d = 0, tot_kd = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = wbase + j * 64 + lane;
+        raws[j] = make_uint2(0u, 0u);
+        rcs[j] = make_int4(0, -1, -1, 0);
+        if (PACK) {
+            if (i < n) raws[j] = reinterpret_cast<const uint2 *>(fr.rec)[i];
+        } else if (i < n) {
+            rcs[j] = fr.rec[i];
+        }
+    }
+    uint32_t kdj[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int i = wbase + j * 64 + lane;
+        if (PACK) rcs[j] = unpack_rec(raws[j]);
+        kdj[j] = (i < n && rcs[j].y >= 0) ? (uint32_t)fr.kdup[i] : 0u;
+    }
+    uint64_t kmm[kPer];  // kept mains
+    uint32_t mkey[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        const int4 rc = rcs[j];
+        const bool has = rc.y >= 0;
+        mkey[j] = f2u((float)((uint32_t)rc.z * 16u + (uint32_t)rc.y) + u2f((uint32_t)rc.x));
+        hasm[j] = __builtin_amdgcn_ballot_w64(has);
+        kmm[j] = __builtin_amdgcn_ballot_w64(has && mkey[j] <= s_theta[key_class(mkey[j])]);
+        incl_d[j] = wave_incl_scan(rec_dups(rc));
+        tot_m += (uint32_t)__popcll(hasm[j]);
+        tot_d += (uint32_t)__builtin_amdgcn_readlane((int)incl_d[j], 63);
+        tot_kd += wave_sum(kdj[j]);
+    }
+    uint32_t tot_km = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) tot_km += (uint32_t)__popcll(kmm[j]);
+    if (lane == 0) s_tot[wid] = make_uint4(tot_m, tot_d, tot_km, tot_kd);
+    __syncthreads();  // (also publishes the zeroed counters and s_theta)
+    uint32_t wm = 0, wd = 0, wkm = 0, wkd = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const uint4 t = s_tot[w];
+        wm += w < wid ? t.x : 0u;
+        wd += w < wid ? t.y : 0u;
+        wkm += w < wid ? t.z : 0u;
+        wkd += w < wid ? t.w : 0u;
+    }
+    uint32_t run_m = off.x + wm, run_d = off.y + wd, run_km = koff.x + wkm, run_kd = koff.y + wkd;
+    uint32_t above = 0, low = 0;
+    // one entry of the walk: its counts, its sample (full position p), its kept store (kpos)
+    auto count = [&](uint32_t key, bool valid, bool kept) {
+        if (!valid) return;
+        const int t = f2i(u2f(key));
+        if ((uint32_t)t < 256u) atomicAdd(&s_tiles[(uint32_t)t * kR + rep], 1u);  // countBins.glsl's int(key)
+        above += key > kKeyCulledBits ? 1u : 0u;
+        low += key < kKey1Bits ? 1u : 0u;
+        if (kept) atomicAdd(&s_kept[key_class(key) * kR + rep], 1u);
+    };
+    auto sample = [&](uint32_t key, uint32_t p) {
+        const uint32_t c = key_class(key);
+        if ((p % kPrefixSample) == 0 && c < 256u && kd.phist)
+            atomicAdd(&kd.phist[((size_t)((p / kPrefixSample) % kPrefixHistCopies) * 256 + c) * kPrefixBuckets +
+                                prefix_slot(prefix_bucket(class_hi(c) - key))],
+                      1u);
+    };
+#pragma unroll 1
+    for (int it = 0; it < kPer; ++it) {
+        int4 rc = rcs[0];
+        uint2 raw = raws[0];
+        uint32_t incl = incl_d[0], key = mkey[0];
+        uint64_t hm = hasm[0], km = kmm[0];
+#pragma unroll
+        for (int j = 1; j < kPer; ++j)
+            if (it == j) {
+                rc = rcs[j];
+                raw = raws[j];
+                incl = incl_d[j];
+                key = mkey[j];
+                hm = hasm[j];
+                km = kmm[j];
+            }
+        const int i = wbase + it * 64 + lane;
+        const bool has = rc.y >= 0;
+        {  // :153-155 the main entry
+            const bool kept = ((km >> lane) & 1ull) != 0;
+            count(key, has, kept);
+            if (has) sample(key, run_m + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u)));
+            const uint32_t kpos = run_km + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
+            if (kept && kpos < cap) {
+                keys[kpos] = key;
+                vals[kpos] = (uint32_t)i;
+            }
+        }
+        run_m += (uint32_t)__popcll(hm);
+        run_km += (uint32_t)__popcll(km);
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (T) {  // uniform per wave: this item's duplicates [V + run_d, + T)
+            s_incl[wid][lane] = (uint16_t)incl;
+            wave_sync_lds();
+            const int ibase = wbase + it * 64;
+            for (uint32_t e0 = 0; e0 < T; e0 += 64) {
+                const uint32_t e = e0 + (uint32_t)lane;
+                int s = 0;  // owner: first lane with incl > e
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (s_incl[wid][s + step - 1] <= e) s += step;
+                const uint32_t q = e - (s ? (uint32_t)s_incl[wid][s - 1] : 0u);
+                const int4 r = PACK ? unpack_rec(make_uint2((uint32_t)__shfl((int)raw.x, s, 64), (uint32_t)__shfl((int)raw.y, s, 64)))
+                                    : make_int4(__shfl(rc.x, s, 64), __shfl(rc.y, s, 64), __shfl(rc.z, s, 64), __shfl(rc.w, s, 64));
+                const int rx0 = r.w & 0xff, rx1 = (r.w >> 8) & 0xff, ry0 = (r.w >> 16) & 0xff, ry1 = (r.w >> 24) & 0xff;
+                const int w = rx1 - rx0 + 1;
+                const bool mainIn = r.y >= rx0 && r.y <= rx1 && r.z >= ry0 && r.z <= ry1;
+                const uint32_t mpos_walk = (uint32_t)((r.z - ry0) * w + (r.y - rx0));
+                const uint32_t k = q + ((mainIn && q >= mpos_walk) ? 1u : 0u);
+                const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(w, 1)));
+                const uint32_t dx = k - dy * (uint32_t)w;
+                const uint32_t tile = (uint32_t)(ry0 + (int)dy) * 16u + (uint32_t)(rx0 + (int)dx);
+                const uint32_t dkey = f2u((float)tile + u2f((uint32_t)r.x));
+                const bool valid = e < T;
+                const bool kept = valid && dkey <= s_theta[key_class(dkey)];
+                const uint64_t kb = __builtin_amdgcn_ballot_w64(kept);
+                count(dkey, valid, kept);
+                if (valid) sample(dkey, V + run_d + e);
+                const uint32_t kpos = KV + run_kd + __builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
+                if (kept && kpos < cap) {
+                    keys[kpos] = dkey;
+                    vals[kpos] = (uint32_t)(ibase + s);
+                }
+                run_kd += (uint32_t)__popcll(kb);
+            }
+            wave_sync_lds();  // s_incl is rewritten by the next item
+        }
+        run_d += T;
+    }
+    above = wave_sum(above);
+    low = wave_sum(low);
+    if (lane == 0) {
+        if (above) atomicAdd(&s_above, above);
+        if (low) atomicAdd(&s_low, low);
+    }
+    __syncthreads();
+    // the workgroup's counts into the copies picked by its id (spread same-address atomics)
+    const uint32_t cp = blockIdx.x % kTileCopyCount;
+    for (int t = threadIdx.x; t < 256; t += kBlock) {
+        const uint32_t c = s_tiles[t * kR] + s_tiles[t * kR + 1] + s_tiles[t * kR + 2] + s_tiles[t * kR + 3];
+        if (c) atomicAdd(&kd.tile_counts[cp * 256 + t], c);
+    }
+    uint32_t *pc = kd.counts + (blockIdx.x % kPrefixCopies) * kClasses;
+    for (int c = threadIdx.x; c < kClasses; c += kBlock) {
+        const uint32_t v = s_kept[c * kR] + s_kept[c * kR + 1] + s_kept[c * kR + 2] + s_kept[c * kR + 3];
+        if (v) atomicAdd(&pc[c], v);
+    }
+    if (threadIdx.x == 0) {
+        if (s_above) atomicAdd(&kd.tile_counts[kTileCopyCount * 256 + cp], s_above);
+        if (s_low) atomicAdd(&kd.counts[kPrefixCopies * kClasses + (blockIdx.x % kPrefixCopies)], s_low);
+    }
+}
+
 // ------------------------------------------------ fused preprocess + emission (frame path)
 // k_pre_emit: one pass over the splats for a frame enqueued without a host round trip.  Each
 // workgroup preprocesses its 1024 splats (wave w: splats [256 w, 256 w + 256) as four items of
@@ -874,11 +1124,6 @@ __device__ __forceinline__ uint64_t lb_load(const uint64_t *p) {
 }
 __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
-    return v;
 }
 
 // KP items of 64 splats per wave (KP * 256 splats per workgroup): 1 for the small scenes it runs
@@ -1900,6 +2145,8 @@ void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, c
 #define GS_PRE(PK, CL)                                                                                                      \
     if (lazy)                                                                                                               \
         hipExtLaunchKernelGGL((k_preprocess_q<PK, CL>), dim3(nb), dim3(64 * kQWaves), 0, s, start, nullptr, 0, P, sc, fr); \
+    else if (fr.theta_in)                                                                                                   \
+        hipExtLaunchKernelGGL((k_preprocess<PK, CL, false, true>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr); \
     else                                                                                                                    \
         hipExtLaunchKernelGGL((k_preprocess<PK, CL, false>), dim3(nb), dim3(kBlock), 0, s, start, nullptr, 0, P, sc, fr)
     if (P.clean) {  // (clean mode always packs its records)
@@ -1914,7 +2161,8 @@ void launch_preprocess(hipStream_t s, const PreParams &P0, const SceneDev &sc, c
 }
 
 void launch_scan_blocksums(hipStream_t s, const FrameDev &fr, int nblocks, hipEvent_t start, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, nblocks);
+    if (fr.theta_in) hipExtLaunchKernelGGL(k_scan_blocksums<true>, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, nblocks);
+    else hipExtLaunchKernelGGL(k_scan_blocksums<false>, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, nblocks);
 }
 
 void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
@@ -1924,13 +2172,20 @@ void launch_emit(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t
     else hipExtLaunchKernelGGL(k_emit<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, prefix_hist);
 }
 
+void launch_emit_kept(hipStream_t s, int n, bool packed, const FrameDev &fr, uint32_t *keys, uint32_t *vals, uint32_t cap,
+                      const KeptDev &kd, hipEvent_t start, hipEvent_t stop) {
+    const dim3 grid(std::max(preprocess_blocks(n), 1));
+    if (packed) hipExtLaunchKernelGGL(k_emit_kept<true>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, kd);
+    else hipExtLaunchKernelGGL(k_emit_kept<false>, grid, dim3(kBlock), 0, s, start, stop, 0, n, fr, keys, vals, cap, kd);
+}
+
 void launch_pre_emit(hipStream_t s, const PreParams &P, const SceneDev &sc, const FrameDev &fr, const LookbackDev &lb,
                      bool lazy, uint32_t *keys, uint32_t *vals, uint32_t cap, uint32_t *prefix_hist, hipEvent_t start,
                      hipEvent_t stop) {
     constexpr int KP = 1;
     const uint32_t nb = (uint32_t)pre_emit_blocks(P.n);
     if (nb == 0) {  // no splats: no entries
-        hipExtLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, 0);
+        hipExtLaunchKernelGGL(k_scan_blocksums<false>, dim3(1), dim3(kScanThreads), 0, s, start, stop, 0, fr, 0);
         return;
     }
     const uint32_t dup_base = (uint32_t)P.n;

@@ -40,7 +40,7 @@ constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
-constexpr int kTileCopies = 16;  // tile counters spread over copies (by workgroup): fewer same-address atomics
+constexpr int kTileCopies = kTileCopyCount;  // tile counters spread over copies (by workgroup): fewer same-address atomics
 
 // GLSL int(float) (countBins.glsl's int(key)): v_cvt_i32_f32 itself (truncate, saturate, NaN -> 0)
 __device__ __forceinline__ int f2i(float f) {
@@ -366,7 +366,8 @@ __device__ void prefix_counts(const uint32_t *__restrict__ tile_counts, const Pr
         }
     }
     __syncthreads();
-    const uint32_t E = elem_count(n_max, cnt);
+    // (the frame's entry count: a kept emission's first pass counts only its kept entries)
+    const uint32_t E = elem_count(pre.cap_all, pre.frame_count ? pre.frame_count : cnt);
     const uint32_t m = t == 0 ? s_low : v;  // keys of class t
     uint32_t tot_m, tot_k;
     const uint32_t P = block_excl_scan_tot<4>(m, s_w, &tot_m);
@@ -383,6 +384,28 @@ __device__ void prefix_counts(const uint32_t *__restrict__ tile_counts, const Pr
         pre.nsel[0] = nsel;
         pre.nsel[1] = 0;
         if (pre.h_slot) pre.h_slot[3] = nsel;  // (above cap_sel: passes 1-3 cannot hold them, the host renders again)
+    }
+    // a kept emission's select wrote the next frame's bounds in two forms (k_prefix_select); the
+    // turned form also holds, per tile, the deepest bound of its 3 x 3 neighbourhood's own bounds
+    // as a depth within the tile: after a turn a tile shows content of its neighbours, whose
+    // saturation depth their own bounds cover, wherever the tile's own list had its entries.
+    // (Neighbours kept whole -- fewer sampled keys than their target -- carry no depth bound.)
+    if (pre.theta_turn && t < 256) {
+        uint32_t b = pre.theta_turn[t];
+        const uint32_t top = class_hi((uint32_t)t) - 1u;
+        const int tx = t & 15, ty = t >> 4;
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int x = tx + dx, y = ty + dy;
+                if (x < 0 || x >= 16 || y < 0 || y >= 16) continue;
+                const uint32_t nc = (uint32_t)(y * 16 + x), th = pre.theta[nc];
+                if (th >= class_hi(nc) - 1u) continue;
+                const float z = __uint_as_float(th) - (float)nc;  // (exact: th in [nc, nc + 1))
+                b = max(b, min(__float_as_uint((float)t + z) + 1u, top));  // (+1 ulp: t + z rounded up)
+            }
+        pre.theta_turn[t] = b;
     }
 }
 
@@ -1327,10 +1350,10 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     // a frame whose camera turned since the frame before (use_depth 0): the depths recorded at the
     // other pose describe content that has moved by a fraction of a tile, so class c takes the
     // deepest of its 3 x 3 tile neighbourhood (with twice the slack) instead of its own
-    uint32_t dep = 0, slack = kPrefixDepthSlack;
-    if (pre.depth && pre.use_depth) {
-        dep = pre.depth[c];
-    } else if (pre.depth && GS_PREFIX_TURN_NB) {
+    // (a kept emission's select, theta_turn set: both bounds, the next frame picks by its own turn)
+    const uint32_t own = pre.depth ? pre.depth[c] : 0u;
+    uint32_t dep_nb = 0;
+    if (pre.depth && GS_PREFIX_TURN_NB && (!pre.use_depth || pre.theta_turn)) {
         const int tx = (int)(c & 15u), ty = (int)(c >> 4);
         constexpr int ry = GS_PREFIX_TURN_NB == 3 ? 0 : 1;  // (3: the row neighbours only)
 #pragma unroll
@@ -1338,10 +1361,10 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
 #pragma unroll
             for (int dx = -1; dx <= 1; ++dx) {
                 const int x = tx + dx, y = ty + dy;
-                if (x >= 0 && x < 16 && y >= 0 && y < 16) dep = max(dep, pre.depth[y * 16 + x]);
+                if (x >= 0 && x < 16 && y >= 0 && y < 16) dep_nb = max(dep_nb, pre.depth[y * 16 + x]);
             }
-        slack = GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack;
     }
+    const uint32_t slack_nb = GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack;
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;
@@ -1358,12 +1381,11 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t ex = block_excl_scan_tot<4>(a, s_w, &tot);
     const uint32_t above = tot - ex - a;  // samples in the buckets of the higher threads
     // the class's target: the configured one, or less where recent blends read the list
-    // shallowly (the depth word was read before the scan's barriers; its decay written after)
-    const uint32_t target = dep ? min(pre.target, 2u * dep + slack) : pre.target;
-    // (decayed by a CAS loop on the current word, not a store of dep - dep / 16: with frames in
+    // shallowly (the depth words were read before the scan's barriers; the decay written after)
+    auto target_of = [&](uint32_t dep, uint32_t slack) { return dep ? min(pre.target, 2u * dep + slack) : pre.target; };
+    // (decayed by a CAS loop on the current word, not a store of own - own / 16: with frames in
     // flight another lane's blend may have raised it since it was read, and a plain store would
     // drop that maximum)
-    const uint32_t own = pre.depth ? (pre.use_depth ? dep : pre.depth[c]) : 0u;
     if (pre.depth && j == 0 && own) {  // (every prefix-sorted frame decays its class's own depth)
         uint32_t cur = own;
         for (int tries = 0; tries < 16; ++tries) {
@@ -1372,26 +1394,33 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
             cur = seen;
         }
     }
-    const uint32_t tgt = (target + kPrefixSample - 1) / kPrefixSample;
     const uint32_t hi = class_hi(c);
-    if (c == 0 && j == 0) pre.theta[256] = 0xffffffffu;  // class 256 is kept whole
-    if (target == 0 || tot < tgt) {
-        if (j == 0) pre.theta[c] = hi - 1u;  // the whole class
-        return;
-    }
-    if (above < tgt && above + a >= tgt) {
-        uint32_t cum = above, b = 0;
-        bool found = false;
-#pragma unroll
-        for (int k = kB - 1; k >= 0; --k) {
-            cum += v[k];
-            if (!found && cum >= tgt) {
-                b = kB * j + (uint32_t)k;
-                found = true;
-            }
+    auto select = [&](uint32_t *theta, uint32_t target) {
+        const uint32_t tgt = (target + kPrefixSample - 1) / kPrefixSample;
+        if (c == 0 && j == 0) theta[256] = 0xffffffffu;  // class 256 is kept whole
+        if (target == 0 || tot < tgt) {
+            if (j == 0) theta[c] = hi - 1u;  // the whole class
+            return;
         }
-        pre.theta[c] = hi - prefix_bucket_dmin(b);
-    }
+        if (above < tgt && above + a >= tgt) {
+            uint32_t cum = above, b = 0;
+            bool found = false;
+#pragma unroll
+            for (int k = kB - 1; k >= 0; --k) {
+                cum += v[k];
+                if (!found && cum >= tgt) {
+                    b = kB * j + (uint32_t)k;
+                    found = true;
+                }
+            }
+            theta[c] = hi - prefix_bucket_dmin(b);
+        }
+    };
+    if (pre.use_depth)
+        select(pre.theta, target_of(own, kPrefixDepthSlack));
+    else
+        select(pre.theta, target_of(dep_nb, slack_nb));
+    if (pre.theta_turn) select(pre.theta_turn, target_of(dep_nb, slack_nb));
 }
 
 __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ keys, const int32_t *__restrict__ order,
@@ -1459,7 +1488,11 @@ void sort_free(SortScratch &sc) {
 
 int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                const uint32_t *dev_count, hipEvent_t start, hipEvent_t stop, uint32_t *bins, bool keys_out,
-               const PrefixDev *pre, int64_t dup_base, bool small, bool bucket) {
+               const PrefixDev *pre, int64_t dup_base, bool small, bool bucket, const KeptSort *kept) {
+    if (kept && (!pre || dup_base >= 0)) {
+        err = "radix sort: a kept emission needs the prefix sort and the contiguous layout";
+        return GS_ERR_INVALID;
+    }
     if (dup_base >= 0 && !dev_count) {
         err = "radix sort: the split layout needs a device count";
         return GS_ERR_INVALID;
@@ -1534,6 +1567,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     uint32_t *kin = keys, *vin = vals, *kout = sc.keys_alt, *vout = sc.vals_alt;
     PrefixDev pd = pre ? *pre : PrefixDev{};
     pd.frame_count = dev_count;
+    pd.cap_all = (uint32_t)n;
     if (pre && kPrefixClassSort) {
         // the prefix sort in one scatter pass and one class sort (k_class_sort): 5 launches
         if (sc.scr_cap < (size_t)n) {
@@ -1572,7 +1606,7 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         return GS_OK;
     }
     const int64_t n_sub = pre ? std::min<int64_t>(n, pre->cap_sel) : n;  // passes 1-3 of a prefix sort
-    if (pre) {  // the class bounds from the keys the emission sampled
+    if (pre) {  // the class bounds from the keys the emission sampled (kept: the next frame's)
         hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
         start = nullptr;
     }
@@ -1586,20 +1620,21 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
 #endif
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
-        const bool big = pass == 0 || all_big;
+        // (a kept emission's first pass reads only the kept keys: the passes-1-3 form and sizes)
+        const bool big = (pass == 0 && !kept) || all_big;
         const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
         // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
-        const uint32_t *cnt = pre && pass > 0 ? pre->nsel : dev_count;
-        const int64_t np = pass > 0 ? n_sub : n;
+        const uint32_t *cnt = pre && pass > 0 ? pre->nsel : kept ? kept->count : dev_count;
+        const int64_t np = pass > 0 || kept ? n_sub : n;
         const uint32_t nb = (uint32_t)((np + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         // the first pass reads the split emission layout (dup_base >= 0), the others their own output
         const uint32_t split = (pass == 0 && dup_base >= 0) ? (uint32_t)dup_base : kNoSplit;
-        if (big && pre)
+        if (big && pre && !kept)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
                                   0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
-        else if (big && bins)
+        else if (big && bins && !kept)  // (a kept emission counted the tiles itself)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
                                   kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
         else if (big && all_big && GS_UPSWEEP_REV)  // (standalone sorts of >= 16M keys)
@@ -1629,10 +1664,13 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
                                                     : k_scan_rows<16, false>;
         hipLaunchKernelGGL(scan, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)np, cnt, tile,
                            sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pmode);
+        // (a kept emission's next frame waits for its bounds: the select's, and their turned form
+        // completed by this scan's class-table workgroup)
+        if (kept && pass == 0 && kept->after_select) (void)hipEventRecord(kept->after_select, s);
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
-        if (big && pre)
+        if (big && pre && !kept)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
                                   e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (big)

@@ -203,7 +203,9 @@ def test_prefix_kept_count_jump():
     ctx.sync()
     psb = ctx.prefix_stats()
     # (B's first frame selects with the per-tile depths A's blends recorded -- another scene's, far
-    # shallower: it may miss, and is then rendered again; never for its kept count)
+    # shallower: it may miss, and is then rendered again; never for its kept count.  With the kept
+    # emission B's first frame keeps every entry and forgets A's depths, so its bounds for the
+    # second frame come from the target alone)
     assert psb["frames"] == 1 and psb["redone"] <= 1, psb
     assert np.array_equal(out.download(np.uint8, W * H * 4), img_b)
     for _ in range(2):
