@@ -224,7 +224,6 @@ struct gs_ctx {
     int theta_cur = 0;
     hipEvent_t theta_ev = nullptr;
     bool theta_valid = false, theta_ev_live = false;
-    bool theta_prev_turned = false;  // the frame before turned (its select's own depths are older)
     const gs_scene *theta_scene = nullptr;
     uint64_t kept_frames = 0;
 };
@@ -1039,9 +1038,13 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 #endif
 constexpr bool kShKept = GS_SH_KEPT != 0;
 
-// prefix-sorted frames of large scenes emit only their kept entries (the bounds of the frame before)
+// 1: prefix-sorted frames of large scenes whose camera did not turn emit only their kept
+// entries (the bounds of the frame before: gs::KeptDev).  Off: bit-exact on the GPU suite, but
+// the work it moves into the preprocess and the emission (+21 and +16 us) costs what the sort
+// saves (-36 us) one frame at a time, and more beside another lane's blend (2175-2196 vs
+// 2344-2355 frames/s, profiles/r05/kept_emission_ab.txt)
 #ifndef GS_KEPT_EMIT
-#define GS_KEPT_EMIT 1
+#define GS_KEPT_EMIT 0
 #endif
 constexpr bool kKeptEmission = GS_KEPT_EMIT != 0;
 
@@ -1329,46 +1332,45 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     // GS_FLAG_SH with the prefix sort: colour only the kept entries' splats, after the sort
     const bool defer_sh = prefix && !fused && (flags & GS_FLAG_SH) && kShKept;
     // the kept emission (gs::KeptDev): a prefix-sorted frame of a large scene, not mostly culled,
-    // emits only the entries at or below the bounds the frame before it selected
-    const bool kept_mode = prefix && !fused && kKeptEmission && !lazy_loads(ctx, scene->n);
+    // whose camera did not turn since the frame before, emits only the entries at or below the
+    // bounds the frame before it selected.  A turned frame emits every entry and selects its own
+    // (its content moved: bounds selected at the other pose missed, tests/test_gpu_prefix.py);
+    // either kind's select writes the bounds the next frame keeps by.
+    const bool kept_base = prefix && !fused && kKeptEmission && !gs::kPrefixClassSort && !lazy_loads(ctx, scene->n);
+    const bool kept_mode = kept_base && !sel_turned;
     const uint32_t *theta_in = nullptr;
-    if (kept_mode) {
+    if (kept_base) {
         for (uint32_t *&t : ctx->theta_buf)
-            if (!t) GS_HIP(ctx, hipMalloc(&t, 2 * gs::kClasses * 4));
+            if (!t) GS_HIP(ctx, hipMalloc(&t, gs::kClasses * 4));
         if (!ctx->theta_ev) GS_HIP(ctx, hipEventCreateWithFlags(&ctx->theta_ev, hipEventDisableTiming));
-        const bool keep_all = !ctx->theta_valid || ctx->theta_scene != scene;
+        const bool keep_all = kept_mode && (!ctx->theta_valid || ctx->theta_scene != scene);
         if (keep_all) {  // no bounds of this scene yet: keep everything
             static std::vector<uint32_t> all = [] {
-                std::vector<uint32_t> a(2 * gs::kClasses);
-                for (int c = 0; c < 256; ++c) a[c] = a[gs::kClasses + c] = gs::class_hi((uint32_t)c) - 1u;
-                a[256] = a[gs::kClasses + 256] = 0xffffffffu;
+                std::vector<uint32_t> a(gs::kClasses);
+                for (int c = 0; c < 256; ++c) a[c] = gs::class_hi((uint32_t)c) - 1u;
+                a[256] = 0xffffffffu;
                 return a;
             }();
             if (ctx->theta_ev_live) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
-            GS_HIP(ctx, hipMemcpyAsync(ctx->theta_buf[ctx->theta_cur], all.data(), 2 * gs::kClasses * 4,
+            GS_HIP(ctx, hipMemcpyAsync(ctx->theta_buf[ctx->theta_cur], all.data(), gs::kClasses * 4,
                                        hipMemcpyHostToDevice, ctx->L->stream));
             // another scene's per-tile depths would size the bounds this frame selects for the
             // next one (which, unlike this frame, cannot hold more): forget them, as a new
             // context starts
             if (ctx->theta_scene && ctx->theta_scene != scene && ctx->prefix_depth)
                 GS_HIP(ctx, hipMemsetAsync(ctx->prefix_depth, 0, 256 * 4, ctx->L->stream));
-            ctx->theta_valid = true;
-            ctx->theta_scene = scene;
-        } else if (ctx->theta_ev_live) {  // the select that wrote them (the frame before, another lane)
+        } else if (kept_mode && ctx->theta_ev_live) {  // the frame before (another lane) wrote them
             GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
         }
-        // the neighbourhood bounds when this frame turned since the frame before, or that frame
-        // did (its select read depths of the pose before it)
-        const bool turned = pd.use_depth == 0;
-        sel_turned = turned || ctx->theta_prev_turned;
-        theta_in = ctx->theta_buf[ctx->theta_cur] + (sel_turned ? gs::kClasses : 0);
-        ctx->theta_prev_turned = turned;
-        // this frame's select: the next frame's bounds, both forms
+        // this frame's select: the bounds of the next frame (and a turned frame's own)
         pd.theta = ctx->theta_buf[ctx->theta_cur ^ 1];
-        pd.theta_turn = pd.theta + gs::kClasses;
-        pd.use_depth = 1;
-        // the sort's four passes sized as passes 1-3 are (a frame keeping every entry: all of them)
-        pd.cap_sel = keep_all ? (uint32_t)ctx->L->e_cap : cap_for(sel_turned);
+        if (kept_mode) {
+            theta_in = ctx->theta_buf[ctx->theta_cur];
+            // the sort's four passes sized as passes 1-3 are (a frame keeping every entry: all)
+            pd.cap_sel = keep_all ? (uint32_t)ctx->L->e_cap : cap_for(false);
+        }
+        ctx->theta_valid = true;
+        ctx->theta_scene = scene;
     } else {
         ctx->theta_valid = false;  // (a frame between them: the bounds would be stale)
     }
@@ -1414,10 +1416,15 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     } else if (!fused && (rc = enqueue_emit(ctx, prefix ? pd.hist : nullptr))) {
         return rc;
     }
+    if (kept_base && !kept_mode) {
+        // a turned frame's select rewrites the bounds the frame before it kept by
+        if (ctx->theta_ev_live) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
+        ks.count = nullptr;
+    }
     if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
-                           ctx->E < ctx->small_sort_entries, kept_mode ? &ks : nullptr)))
+                           ctx->E < ctx->small_sort_entries, kept_base ? &ks : nullptr)))
         return rc;
-    if (kept_mode) {  // the next kept frame reads the bounds this frame's select writes
+    if (kept_base) {  // the next frame reads the bounds this frame's select writes
         ctx->theta_cur ^= 1;
         ctx->theta_ev_live = true;
     }

@@ -103,9 +103,6 @@ struct PrefixDev {
     int32_t use_depth;  // 0: the camera turned since the frame before (the depths describe another
                         // view): each class takes its tile neighbourhood's deepest depth
                         // (GS_PREFIX_TURN_NB); its blend still records them
-    // a kept emission's select (theta: the next frame's bounds, with the own depths): the bounds
-    // for a next frame that turned (the neighbourhood form) here [kClasses], else null
-    uint32_t *theta_turn;
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
 };
@@ -203,9 +200,12 @@ struct SortScratch {
 // dup_base >= 0 (with dev_count): the input is k_pre_emit's split layout, V = dev_count[0] mains
 // at [0, V) and the dev_count[1] duplicates at [dup_base, dup_base + D); the first pass reads it
 // as one array of V + D entries (n is then the capacity of that virtual array).
-// kept != null (with pre): the input is a kept emission (k_emit_kept): kept->count[0] + [1] entries,
-// already filtered by the class bounds and counted (tile counts, kept per class); the select
-// writes the NEXT frame's bounds (pre->theta) and kept->after_select is recorded behind it
+// kept != null (with pre), kept->count set: the input is a kept emission (k_emit_kept):
+// kept->count[0] + [1] entries, already filtered by the class bounds and counted (tile counts,
+// kept per class); the select writes the NEXT frame's bounds (pre->theta), and
+// kept->after_select is recorded behind the first pass's scan (its last read of the bounds this
+// frame kept by).  kept->count null: a full emission, after_select recorded behind the select
+// (whose bounds a kept frame after this one reads)
 struct KeptSort {
     const uint32_t *count;
     hipEvent_t after_select;

@@ -926,6 +926,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_kept(int n, FrameDev fr, uint32
     for (int c = threadIdx.x; c < 256 * kR; c += kBlock) s_tiles[c] = 0;
     for (int c = threadIdx.x; c < kClasses * kR; c += kBlock) s_kept[c] = 0;
     if (threadIdx.x == 0) s_above = s_low = 0;
+    __syncthreads();  // s_theta (the kept ballots below read it) and the zeroed counters
     const uint2 off = fr.blocksum[blockIdx.x], koff = fr.blocksum_k[blockIdx.x];
     const uint32_t V = fr.totals[0], KV = fr.totals[2];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
@@ -972,7 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_emit_kept(int n, FrameDev fr, uint32
 #pragma unroll
     for (int j = 0; j < kPer; ++j) tot_km += (uint32_t)__popcll(kmm[j]);
     if (lane == 0) s_tot[wid] = make_uint4(tot_m, tot_d, tot_km, tot_kd);
-    __syncthreads();  // (also publishes the zeroed counters and s_theta)
+    __syncthreads();
     uint32_t wm = 0, wd = 0, wkm = 0, wkd = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; ++w) {

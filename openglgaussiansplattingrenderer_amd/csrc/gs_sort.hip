@@ -385,28 +385,6 @@ __device__ void prefix_counts(const uint32_t *__restrict__ tile_counts, const Pr
         pre.nsel[1] = 0;
         if (pre.h_slot) pre.h_slot[3] = nsel;  // (above cap_sel: passes 1-3 cannot hold them, the host renders again)
     }
-    // a kept emission's select wrote the next frame's bounds in two forms (k_prefix_select); the
-    // turned form also holds, per tile, the deepest bound of its 3 x 3 neighbourhood's own bounds
-    // as a depth within the tile: after a turn a tile shows content of its neighbours, whose
-    // saturation depth their own bounds cover, wherever the tile's own list had its entries.
-    // (Neighbours kept whole -- fewer sampled keys than their target -- carry no depth bound.)
-    if (pre.theta_turn && t < 256) {
-        uint32_t b = pre.theta_turn[t];
-        const uint32_t top = class_hi((uint32_t)t) - 1u;
-        const int tx = t & 15, ty = t >> 4;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int x = tx + dx, y = ty + dy;
-                if (x < 0 || x >= 16 || y < 0 || y >= 16) continue;
-                const uint32_t nc = (uint32_t)(y * 16 + x), th = pre.theta[nc];
-                if (th >= class_hi(nc) - 1u) continue;
-                const float z = __uint_as_float(th) - (float)nc;  // (exact: th in [nc, nc + 1))
-                b = max(b, min(__float_as_uint((float)t + z) + 1u, top));  // (+1 ulp: t + z rounded up)
-            }
-        pre.theta_turn[t] = b;
-    }
 }
 
 // The prefix sort's draw limits (the bins workgroup of the last pass): the bins, then per tile
@@ -1350,10 +1328,9 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     // a frame whose camera turned since the frame before (use_depth 0): the depths recorded at the
     // other pose describe content that has moved by a fraction of a tile, so class c takes the
     // deepest of its 3 x 3 tile neighbourhood (with twice the slack) instead of its own
-    // (a kept emission's select, theta_turn set: both bounds, the next frame picks by its own turn)
     const uint32_t own = pre.depth ? pre.depth[c] : 0u;
     uint32_t dep_nb = 0;
-    if (pre.depth && GS_PREFIX_TURN_NB && (!pre.use_depth || pre.theta_turn)) {
+    if (pre.depth && GS_PREFIX_TURN_NB && !pre.use_depth) {
         const int tx = (int)(c & 15u), ty = (int)(c >> 4);
         constexpr int ry = GS_PREFIX_TURN_NB == 3 ? 0 : 1;  // (3: the row neighbours only)
 #pragma unroll
@@ -1420,7 +1397,6 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
         select(pre.theta, target_of(own, kPrefixDepthSlack));
     else
         select(pre.theta, target_of(dep_nb, slack_nb));
-    if (pre.theta_turn) select(pre.theta_turn, target_of(dep_nb, slack_nb));
 }
 
 __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ keys, const int32_t *__restrict__ order,
@@ -1606,6 +1582,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         return GS_OK;
     }
     const int64_t n_sub = pre ? std::min<int64_t>(n, pre->cap_sel) : n;  // passes 1-3 of a prefix sort
+    // a kept emission's input (kept->count set); else kept->after_select alone (see KeptSort)
+    const bool kept_in = kept && kept->count;
     if (pre) {  // the class bounds from the keys the emission sampled (kept: the next frame's)
         hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
         start = nullptr;
@@ -1621,20 +1599,20 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     for (int pass = 0; pass < 4; ++pass) {
         const int shift = 8 * pass;
         // (a kept emission's first pass reads only the kept keys: the passes-1-3 form and sizes)
-        const bool big = (pass == 0 && !kept) || all_big;
+        const bool big = (pass == 0 && !kept_in) || all_big;
         const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
         // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
-        const uint32_t *cnt = pre && pass > 0 ? pre->nsel : kept ? kept->count : dev_count;
-        const int64_t np = pass > 0 || kept ? n_sub : n;
+        const uint32_t *cnt = pre && pass > 0 ? pre->nsel : kept_in ? kept->count : dev_count;
+        const int64_t np = pass > 0 || kept_in ? n_sub : n;
         const uint32_t nb = (uint32_t)((np + tile - 1) / tile);  // tiles of this pass = hist row stride
         // timing events on the first and last dispatch (see launch_preprocess)
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         // the first pass reads the split emission layout (dup_base >= 0), the others their own output
         const uint32_t split = (pass == 0 && dup_base >= 0) ? (uint32_t)dup_base : kNoSplit;
-        if (big && pre && !kept)
+        if (big && pre && !kept_in)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
                                   0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
-        else if (big && bins && !kept)  // (a kept emission counted the tiles itself)
+        else if (big && bins && !kept_in)  // (a kept emission counted the tiles itself)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
                                   kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
         else if (big && all_big && GS_UPSWEEP_REV)  // (standalone sorts of >= 16M keys)
@@ -1664,13 +1642,12 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
                                                     : k_scan_rows<16, false>;
         hipLaunchKernelGGL(scan, dim3(kRadix + (with_bins ? 1 : 0)), dim3(256), 0, s, sc.hist, nb, (uint32_t)np, cnt, tile,
                            sc.row_total, tile_counts, with_bins ? bins : nullptr, pd, pmode);
-        // (a kept emission's next frame waits for its bounds: the select's, and their turned form
-        // completed by this scan's class-table workgroup)
-        if (kept && pass == 0 && kept->after_select) (void)hipEventRecord(kept->after_select, s);
+        // (a kept emission's next frame waits for its bounds, and for this pass's reads of them)
+        if (kept_in && pass == 0 && kept->after_select) (void)hipEventRecord(kept->after_select, s);
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
-        if (big && pre && !kept)
+        if (big && pre && !kept_in)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
                                   e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (big)
@@ -1688,6 +1665,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         else
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPackIn>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr,
                                   e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
+        // (a full emission's first pass kept its keys by the bounds its select wrote: the frame
+        // after it, which keeps by the same bounds and then rewrites the other buffer, waits)
+        if (kept && !kept_in && pass == 0 && kept->after_select) (void)hipEventRecord(kept->after_select, s);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }

@@ -71,6 +71,33 @@ def test_prefix_c3_frames_equal_full_sort(c3, oracle, flags):
     assert np.array_equal(sp.read(g.GS_READ_BINS, 256), o["bins"])
 
 
+def test_prefix_kept_frames_across_modes(c3):
+    """Phases of static prefix-sorted frames (ref mode, clean mode, ref mode again, each after a
+    synchronous frame; each phase's bounds sized by the other mode's per-tile depths): no frame
+    rendered again, every one bit-exact against the phase's synchronous frame.  (Under the
+    opt-in kept emission, GS_KEPT_EMIT=1, a race on its bounds in LDS once gave wrong images
+    here without a miss.)"""
+    ctx, sp = c3
+    W, H = 1920, 1080
+    u = g.main_camera(W, H).uniforms()
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(6)]
+    assert ctx.set_sort_prefix() == 32768
+    for flags in [0, g.GS_FLAG_CLEAN, 0, g.GS_FLAG_CLEAN]:
+        sp.flags = flags
+        render_sync(sp, u, ref)
+        img = ref.download(np.uint8, W * H * 4)
+        ctx.prefix_stats(reset=True)
+        for o in outs:
+            render_spec(sp, u, o)
+        ctx.sync()
+        ps = ctx.prefix_stats()
+        assert ps["frames"] == len(outs) and ps["redone"] == 0, (flags, ps)
+        for k, o in enumerate(outs):
+            assert np.array_equal(o.download(np.uint8, W * H * 4), img), (flags, k)
+    sp.flags = 0
+
+
 def test_prefix_misses_render_again():
     """A prefix far too shallow: the blend reaches unsorted positions, the frames are rendered
     again with the full sort (and the depth doubles) -- every image still equals the
