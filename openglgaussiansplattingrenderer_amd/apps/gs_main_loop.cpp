@@ -31,6 +31,9 @@ int main(int argc, char **argv) {
     gs::Context ctx(0);
     if (!ctx.get()) return 3;
     if (ctx.setLanes(lanes) < 0) return 3;
+    // one timestamp per frame, as main.cpp:52-58's GL_TIMESTAMP queries (the library's default
+    // times every stage boundary, whose events idle the stream a few microseconds each)
+    if (gs_timing_enable(ctx.get(), GS_TIMING_FRAME) != GS_OK) return 3;
     // main.cpp:40-45
     gs::Camera camera(5.0f, 0.5f, -4.0f);
     camera.rotateDown(20.0f);
