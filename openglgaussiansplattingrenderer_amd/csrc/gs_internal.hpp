@@ -115,6 +115,14 @@ constexpr uint32_t kPrefixDepthSlack = GS_PREFIX_SLACK;
 #ifndef GS_PREFIX_TURN_NB
 #define GS_PREFIX_TURN_NB 1
 #endif
+// a turned frame's class target: GS_PREFIX_TURN_MUL x the neighbourhood's depth + its slack x
+// GS_PREFIX_TURN_SLACK_MUL
+#ifndef GS_PREFIX_TURN_MUL
+#define GS_PREFIX_TURN_MUL 2u
+#endif
+#ifndef GS_PREFIX_TURN_SLACK_MUL
+#define GS_PREFIX_TURN_SLACK_MUL 1u
+#endif
 constexpr uint32_t kKey1Bits = 0x3f800000u;    // bits(1.0f)
 constexpr uint32_t kKey256Bits = 0x43800000u;  // bits(256.0f)
 // key class: t for the keys in [t, t+1), t < 256; 256 for every other bit pattern

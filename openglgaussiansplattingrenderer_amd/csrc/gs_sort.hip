@@ -1341,7 +1341,7 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
                 if (x >= 0 && x < 16 && y >= 0 && y < 16) dep_nb = max(dep_nb, pre.depth[y * 16 + x]);
             }
     }
-    const uint32_t slack_nb = GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack;
+    const uint32_t slack_nb = (GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack) * GS_PREFIX_TURN_SLACK_MUL;
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;
@@ -1359,7 +1359,7 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
     const uint32_t above = tot - ex - a;  // samples in the buckets of the higher threads
     // the class's target: the configured one, or less where recent blends read the list
     // shallowly (the depth words were read before the scan's barriers; the decay written after)
-    auto target_of = [&](uint32_t dep, uint32_t slack) { return dep ? min(pre.target, 2u * dep + slack) : pre.target; };
+    auto target_of = [&](uint32_t dep, uint32_t slack, uint32_t mul) { return dep ? min(pre.target, mul * dep + slack) : pre.target; };
     // (decayed by a CAS loop on the current word, not a store of own - own / 16: with frames in
     // flight another lane's blend may have raised it since it was read, and a plain store would
     // drop that maximum)
@@ -1394,9 +1394,9 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
         }
     };
     if (pre.use_depth)
-        select(pre.theta, target_of(own, kPrefixDepthSlack));
+        select(pre.theta, target_of(own, kPrefixDepthSlack, 2u));
     else
-        select(pre.theta, target_of(dep_nb, slack_nb));
+        select(pre.theta, target_of(dep_nb, slack_nb, GS_PREFIX_TURN_MUL));
 }
 
 __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ keys, const int32_t *__restrict__ order,
