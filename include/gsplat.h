@@ -129,6 +129,13 @@ int gs_ctx_set_small_limits(gs_ctx *ctx, int64_t draw_entries, int64_t sort_entr
  * scatter by int(key), then LSD passes per tile in LDS); 0 = four 8-bit passes (8 launches);
  * -1 leaves it.  Returns the form now set (or a negative GS_ERR_*).  Same result either way. */
 int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on);
+/* The kept emission of prefix-sorted frames (large scenes, frames enqueued without a round trip
+ * whose camera did not turn since the frame before): the preprocess counts and the emission
+ * writes only the entries at or below the key bounds the frame before selected, and the sort's
+ * four passes run on those alone.  1 = on, 0 = off (default: measured slower),
+ * -1 leaves it; *kept_frames (may be null) = frames emitted that way so far.  Returns the
+ * setting (or a negative GS_ERR_*).  Images are the same either way. */
+int gs_ctx_set_kept_emission(gs_ctx *ctx, int on, uint64_t *kept_frames);
 /* The fused preprocess + emission of small scenes (<= 64k splats, frames enqueued without a host
  * round trip) places each workgroup's entries by a decoupled look-back over the workgroups before
  * it.  A wait for a predecessor is bounded (default 2^15 polls); a workgroup that gives up emits

@@ -116,6 +116,7 @@ SIGNATURES = {
     "gs_ctx_set_draw_sub": (_i, [_vp, _i, ctypes.POINTER(_i)]),
     "gs_ctx_set_small_limits": (_i, [_vp, ctypes.c_int64, ctypes.c_int64]),
     "gs_ctx_set_bucket_sort": (_i, [_vp, _i]),
+    "gs_ctx_set_kept_emission": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_uint64)]),
     "gs_ctx_set_lookback_spin": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_uint64)]),
     "gs_prefix_stats": (_i, [_vp, _vp, _i]),
     "gs_malloc": (_i, [_vp, _sz, ctypes.POINTER(_vp)]),

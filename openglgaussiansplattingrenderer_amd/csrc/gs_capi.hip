@@ -56,6 +56,14 @@ constexpr int kPrefixCooldown = 64;
 #define GS_PREFIX_TURN_MDEG 250
 #endif
 const float kPrefixTurnCos = (float)std::cos(GS_PREFIX_TURN_MDEG * 1e-3 * 3.14159265358979323846 / 180.0);
+// the default of gs_ctx_set_kept_emission: off.  Prefix-sorted frames of large scenes whose
+// camera did not turn would emit only their kept entries (the bounds of the frame before:
+// gs::KeptDev) -- bit-exact, but the work it moves into the preprocess and the emission (+21 and
+// +16 us) costs what the sort saves (-36 us) one frame at a time, and more beside another lane's
+// blend (2175-2196 vs 2344-2355 frames/s, profiles/r05/kept_emission_ab.txt)
+#ifndef GS_KEPT_EMIT
+#define GS_KEPT_EMIT 0
+#endif
 // cos of the rotation between two view matrices: (trace(R1^T R2) - 1) / 2 over their upper-left
 // 3x3 blocks (the same index set in either storage order)
 static float turn_cos(const float *a, const float *b) {
@@ -226,6 +234,7 @@ struct gs_ctx {
     bool theta_valid = false, theta_ev_live = false;
     const gs_scene *theta_scene = nullptr;
     uint64_t kept_frames = 0;
+    bool kept_emit = GS_KEPT_EMIT != 0;  // gs_ctx_set_kept_emission
 };
 
 struct gs_scene {
@@ -1038,15 +1047,6 @@ int check_frame_args(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, c
 #endif
 constexpr bool kShKept = GS_SH_KEPT != 0;
 
-// 1: prefix-sorted frames of large scenes whose camera did not turn emit only their kept
-// entries (the bounds of the frame before: gs::KeptDev).  Off: bit-exact on the GPU suite, but
-// the work it moves into the preprocess and the emission (+21 and +16 us) costs what the sort
-// saves (-36 us) one frame at a time, and more beside another lane's blend (2175-2196 vs
-// 2344-2355 frames/s, profiles/r05/kept_emission_ab.txt)
-#ifndef GS_KEPT_EMIT
-#define GS_KEPT_EMIT 0
-#endif
-constexpr bool kKeptEmission = GS_KEPT_EMIT != 0;
 
 #ifndef GS_QUEUE_FRAC
 #define GS_QUEUE_FRAC 2  // the queued preprocess when fewer than n / GS_QUEUE_FRAC splats were visible
@@ -1336,7 +1336,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     // bounds the frame before it selected.  A turned frame emits every entry and selects its own
     // (its content moved: bounds selected at the other pose missed, tests/test_gpu_prefix.py);
     // either kind's select writes the bounds the next frame keeps by.
-    const bool kept_base = prefix && !fused && kKeptEmission && !gs::kPrefixClassSort && !lazy_loads(ctx, scene->n);
+    const bool kept_base = prefix && !fused && ctx->kept_emit && !gs::kPrefixClassSort && !lazy_loads(ctx, scene->n);
     const bool kept_mode = kept_base && !sel_turned;
     const uint32_t *theta_in = nullptr;
     if (kept_base) {
@@ -1652,6 +1652,16 @@ int gs_ctx_set_bucket_sort(gs_ctx *ctx, int on) {
     if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
     if (on >= 0) ctx->bucket_sort = on != 0;
     return ctx->bucket_sort ? 1 : 0;
+}
+
+int gs_ctx_set_kept_emission(gs_ctx *ctx, int on, uint64_t *kept_frames) {
+    if (!ctx) return set_error(nullptr, GS_ERR_INVALID, "ctx is null");
+    if (on >= 0 && (on != 0) != ctx->kept_emit) {
+        ctx->kept_emit = on != 0;
+        ctx->theta_valid = false;  // (the next kept frame starts from every entry)
+    }
+    if (kept_frames) *kept_frames = ctx->kept_frames;
+    return ctx->kept_emit ? 1 : 0;
 }
 
 int gs_ctx_set_lookback_spin(gs_ctx *ctx, int limit, uint64_t *redone) {

@@ -35,6 +35,11 @@ constexpr int kWaveTile = 64 * kItems;        // 1024 keys per wave
 #endif
 constexpr int kWaveSmall = GS_WAVE_SMALL, kWaveBig = GS_WAVE_BIG;   // waves per workgroup: passes 1-3 / pass 0
 constexpr int kTileSmall = kWaveSmall * kWaveTile;  // 4096
+// waves per workgroup of a frame's prefix-sort first pass (its downsweep's LDS holds a whole tile)
+#ifndef GS_PREFIX_P0_WAVES
+#define GS_PREFIX_P0_WAVES GS_WAVE_BIG
+#endif
+constexpr int kP0Waves = GS_PREFIX_P0_WAVES;
 constexpr int kRadix = 256;
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
@@ -1600,7 +1605,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const int shift = 8 * pass;
         // (a kept emission's first pass reads only the kept keys: the passes-1-3 form and sizes)
         const bool big = (pass == 0 && !kept_in) || all_big;
-        const uint32_t tile = big ? kWaveBig * kWaveTile : kTileSmall;
+        // (a prefix sort's first pass keeps ~1 key in 8: its tiles of kP0Waves waves)
+        const bool p0 = big && pre && !kept_in;
+        const uint32_t tile = p0 ? kP0Waves * kWaveTile : big ? kWaveBig * kWaveTile : kTileSmall;
         // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
         const uint32_t *cnt = pre && pass > 0 ? pre->nsel : kept_in ? kept->count : dev_count;
         const int64_t np = pass > 0 || kept_in ? n_sub : n;
@@ -1609,8 +1616,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 3 ? stop : nullptr;
         // the first pass reads the split emission layout (dup_base >= 0), the others their own output
         const uint32_t split = (pass == 0 && dup_base >= 0) ? (uint32_t)dup_base : kNoSplit;
-        if (big && pre && !kept_in)
-            hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr,
+        if (p0)
+            hipExtLaunchKernelGGL((k_upsweep<kP0Waves, true, true>), dim3(xcd_grid(nb)), dim3(kP0Waves * 64), 0, s, e0, nullptr,
                                   0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, tile_counts, pd, split);
         else if (big && bins && !kept_in)  // (a kept emission counted the tiles itself)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
@@ -1647,8 +1654,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         // keys_out false: pass 2 packs (top key byte, value), pass 3 unpacks the values only;
         // a prefix sort moves pairs and places the values in its last pass
         const int fmt = pre ? (pass == 3 ? kPlace : kPairs) : keys_out || pass < 2 ? kPairs : pass == 2 ? kPackOut : kPackIn;
-        if (big && pre && !kept_in)
-            hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr,
+        if (p0)
+            hipExtLaunchKernelGGL((k_downsweep<kP0Waves, kPairs, true>), dim3(xcd_grid(nb)), dim3(kP0Waves * 64), 0, s, nullptr,
                                   e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (big)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,

@@ -73,6 +73,15 @@ class Context:
         check(min(r, 0), self.handle)
         return r
 
+    def set_kept_emission(self, on: int = -1):
+        """gs_ctx_set_kept_emission: prefix-sorted frames emit and sort only the entries within
+        the previous frame's key bounds (1) or every entry (0, default); -1 leaves it.  Returns
+        (setting, frames emitted that way so far)."""
+        n = ctypes.c_uint64()
+        r = lib().gs_ctx_set_kept_emission(self.handle, int(on), ctypes.byref(n))
+        check(min(r, 0), self.handle)
+        return r, int(n.value)
+
     def set_lookback_spin(self, limit: int = -1):
         """gs_ctx_set_lookback_spin: polls the fused preprocess + emission's look-back waits before
         it gives up and the frame is rendered again (0: at once, a test hook; -1 leaves it).

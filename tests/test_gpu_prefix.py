@@ -71,18 +71,22 @@ def test_prefix_c3_frames_equal_full_sort(c3, oracle, flags):
     assert np.array_equal(sp.read(g.GS_READ_BINS, 256), o["bins"])
 
 
-def test_prefix_kept_frames_across_modes(c3):
+@pytest.mark.parametrize("kept", [0, 1])
+def test_prefix_kept_frames_across_modes(c3, kept):
     """Phases of static prefix-sorted frames (ref mode, clean mode, ref mode again, each after a
     synchronous frame; each phase's bounds sized by the other mode's per-tile depths): no frame
-    rendered again, every one bit-exact against the phase's synchronous frame.  (Under the
-    opt-in kept emission, GS_KEPT_EMIT=1, a race on its bounds in LDS once gave wrong images
-    here without a miss.)"""
+    rendered again, every one bit-exact against the phase's synchronous frame -- with the full
+    emission and with the kept emission (gs_ctx_set_kept_emission: each frame after a phase's
+    first emits only the entries within the previous frame's bounds; a race on those bounds in
+    LDS once gave wrong images here without a miss)."""
     ctx, sp = c3
     W, H = 1920, 1080
     u = g.main_camera(W, H).uniforms()
     ref = g.DeviceBuffer(ctx, W * H * 4)
     outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(6)]
     assert ctx.set_sort_prefix() == 32768
+    assert ctx.set_kept_emission(kept)[0] == kept
+    k0 = ctx.set_kept_emission()[1]
     for flags in [0, g.GS_FLAG_CLEAN, 0, g.GS_FLAG_CLEAN]:
         sp.flags = flags
         render_sync(sp, u, ref)
@@ -95,7 +99,44 @@ def test_prefix_kept_frames_across_modes(c3):
         assert ps["frames"] == len(outs) and ps["redone"] == 0, (flags, ps)
         for k, o in enumerate(outs):
             assert np.array_equal(o.download(np.uint8, W * H * 4), img), (flags, k)
+    assert ctx.set_kept_emission(0)[1] - k0 == (4 * len(outs) if kept else 0)
     sp.flags = 0
+
+
+def test_prefix_kept_emission_turning_camera():
+    """The kept emission under a camera turning 3 degrees per frame and walking 0.1 per frame:
+    turned frames emit every entry and select their own bounds, the frames after them keep by
+    those; every image bit-exact against the host-synchronous full sort, at most one frame
+    rendered again."""
+    W, H = 1920, 1080
+    ctx = g.Context(0)
+    sp = g.Splats.from_raw(*bicycle_standin_raw(), W, H, ctx=ctx)
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+
+    def cam(k):
+        c = g.main_camera(W, H)
+        c.rotateRight(3.0 * min(k, 4))  # turn for 4 frames, then walk
+        c.moveForward(0.1 * max(0, k - 4))
+        return c.uniforms()
+
+    render_sync(sp, cam(0), ref)
+    assert ctx.set_sort_prefix() == 32768
+    assert ctx.set_kept_emission(1)[0] == 1
+    ctx.prefix_stats(reset=True)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    got = []
+    for k in range(9):
+        render_spec(sp, cam(k), outs[k % 3])
+        if k % 3 == 2:
+            ctx.sync()
+            got += [o.download(np.uint8, W * H * 4) for o in outs]
+    ps = ctx.prefix_stats()
+    assert ps["frames"] == 9 and ps["redone"] <= 1, ps
+    assert ctx.set_kept_emission()[1] >= 4  # the walking frames kept
+    for k in range(9):
+        render_sync(sp, cam(k), ref)
+        assert np.array_equal(got[k], ref.download(np.uint8, W * H * 4)), f"frame {k}"
+    ctx.close()
 
 
 def test_prefix_misses_render_again():
