@@ -193,6 +193,11 @@ struct SortScratch {
     uint32_t *bkt = nullptr;       // [2][256]: the bucket form's bucket bases and counts
     uint32_t *vals_scr = nullptr;  // the prefix class sort's scratch values (long buckets)
     size_t scr_cap = 0;
+    // GS_SORT11 (standalone sorts of >= 16M pairs in three passes of 11/11/10-bit digits): the
+    // [2048][nb] histograms, the row totals, and a second alternate pair array (three passes:
+    // keys -> alt -> alt2 -> keys)
+    uint32_t *hist11 = nullptr, *row11 = nullptr, *keys_alt2 = nullptr, *vals_alt2 = nullptr;
+    size_t hist11_cap = 0, alt2_cap = 0;
 };
 
 // Stable sort of (key, value) pairs: n elements, or -- when dev_count is given -- min(n,

@@ -1412,6 +1412,206 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 }  // namespace
 
+// ---------------------------------------------------------------- GS_SORT11 (opt-in)
+// Standalone sorts of >= 16M pairs in three LSD passes of 11, 11 and 10 bits (VERDICT r4 item 5:
+// 4 + 3 x 16 bytes of pairs per key against 4 x 16 + 4), reduce-then-scan as the 8-bit passes:
+// k_upsweep11 (a 2048-bin histogram per 8192-key tile), k_scan_rows over the 2048 rows,
+// k_downsweep11 (stable ranking by an 11-bit match, the tile reordered in LDS, coalesced
+// scatter).  The per-wave digit counters and the reorder buffer share the LDS (positions are
+// kept in registers across the barrier): 80 KB, two workgroups per CU.
+#ifndef GS_SORT11
+#define GS_SORT11 0
+#endif
+constexpr int kR11 = 2048;
+template <int BITS>
+__device__ __forceinline__ uint64_t match_digit_n(uint32_t d, uint64_t active) {
+    uint32_t xlo = 0, xhi = 0;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        uint32_t sb = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
+        asm volatile("" : "+v"(sb));
+        const uint64_t bb = __ballot(sb != 0u);
+        xlo = or_xor(xlo, sb, (uint32_t)bb);
+        xhi = or_xor(xhi, sb, (uint32_t)(bb >> 32));
+    }
+    return (((uint64_t)~xhi << 32) | ~xlo) & active;
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kWaveBig * 64) void k_upsweep11(const uint32_t *__restrict__ keys, uint32_t n, int shift,
+                                                             uint32_t *__restrict__ hist, uint32_t nb) {
+    constexpr int kThreads = kWaveBig * 64, kTile = kThreads * kItems, R = 1 << BITS;
+    const uint32_t live = (n + kTile - 1) / kTile;
+    const uint32_t tile = xcd_tile_rev(live);
+    if (tile >= live) return;  // uniform
+    __shared__ uint32_t s_cnt[R];
+    for (int i = threadIdx.x; i < R; i += kThreads) s_cnt[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        kk[k] = idx < n ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+        if (base + k * 64 < n) atomicAdd(&s_cnt[(kk[k] >> shift) & (R - 1)], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < R; d += kThreads) hist[(size_t)d * nb + tile] = s_cnt[d];
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kWaveBig * 64) void k_downsweep11(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                               uint32_t n, int shift, const uint32_t *__restrict__ hist,
+                                                               uint32_t nb, const uint32_t *__restrict__ row_total) {
+    constexpr int W = kWaveBig, kThreads = W * 64, kTile = kThreads * kItems, R = 1 << BITS;
+    static_assert(W * kR11 * 4 >= kTile * 8, "the reorder buffer fits in the counters' LDS");
+    const uint32_t live = (n + kTile - 1) / kTile;
+    const uint32_t tile = xcd_tile(live);
+    if (tile >= live) return;  // uniform
+    __shared__ uint32_t s_cnt[W][kR11];  // per-wave counters (R used), then the tile's keys and values
+    __shared__ uint32_t s_start[R];
+    __shared__ int32_t s_gbase[R];
+    __shared__ uint32_t s_w[W];
+    uint32_t *s_keys = &s_cnt[0][0], *s_vals = &s_cnt[0][0] + kTile;
+    for (int i = threadIdx.x; i < W * kR11; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint32_t tile0 = tile * (uint32_t)kTile;
+    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
+    uint32_t kk[kItems], vv[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t idx = base + k * 64;
+        kk[k] = idx < n ? kin[idx] : 0u;
+        vv[k] = idx < n ? vin[idx] : 0u;
+    }
+    uint32_t rank[kItems], lead[kItems], old[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const bool valid = base + k * 64 < n;
+        const uint32_t d = (kk[k] >> shift) & (R - 1);
+        const uint64_t m = match_digit_n<BITS>(d, __ballot(valid));
+        rank[k] = count_below(m);
+        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
+        old[k] = valid ? (uint32_t)__popcll(m) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+        if (base + k * 64 < n && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & (R - 1)], old[k]);
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    __syncthreads();
+    // per digit: the waves' exclusive offsets, the tile's digit starts, the global bases
+    constexpr int DPT = R / kThreads;  // digits per thread (4 or 2)
+    uint32_t tot[DPT], a = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+        const int d = threadIdx.x * DPT + j;
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t c = s_cnt[w][d];
+            s_cnt[w][d] = t;
+            t += c;
+        }
+        tot[j] = t;
+        a += t;
+    }
+    const uint32_t ex = block_excl_scan<W>(a, s_w);
+    uint32_t g = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) g += row_total[threadIdx.x * DPT + j];
+    const uint32_t gex = block_excl_scan<W>(g, s_w);
+    {
+        uint32_t st = ex, gb = gex;
+#pragma unroll
+        for (int j = 0; j < DPT; ++j) {
+            const int d = threadIdx.x * DPT + j;
+            s_start[d] = st;
+            s_gbase[d] = (int32_t)(gb + hist[(size_t)d * nb + tile]) - (int32_t)st;
+            st += tot[j];
+            gb += row_total[d];
+        }
+    }
+    __syncthreads();
+    uint32_t pos[kItems];
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+        const uint32_t d = (kk[k] >> shift) & (R - 1);
+        pos[k] = s_start[d] + s_cnt[wid][d] + rank[k];
+    }
+    __syncthreads();  // (the counters' LDS becomes the reorder buffer)
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+        if (base + k * 64 < n) {
+            s_keys[pos[k]] = kk[k];
+            s_vals[pos[k]] = vv[k];
+        }
+    __syncthreads();
+    const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
+    for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
+        const uint32_t key = s_keys[i];
+        const uint32_t o = (uint32_t)(s_gbase[(key >> shift) & (R - 1)] + (int32_t)i);
+        kout[o] = key;
+        vout[o] = s_vals[i];
+    }
+}
+
+int sort_pairs11(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
+                 hipEvent_t start, hipEvent_t stop) {
+    constexpr uint32_t kTile = kWaveBig * kWaveTile;
+    const uint32_t nb = (uint32_t)((n + kTile - 1) / kTile);
+    if ((size_t)n > sc.alt2_cap || (size_t)nb * kR11 > sc.hist11_cap) {
+        (void)hipStreamSynchronize(s);
+        for (uint32_t **p : {&sc.keys_alt2, &sc.vals_alt2, &sc.hist11})
+            if (*p) (void)hipFree(*p), *p = nullptr;
+        sc.alt2_cap = sc.hist11_cap = 0;
+        if (hipMalloc(&sc.keys_alt2, (size_t)n * 4) != hipSuccess || hipMalloc(&sc.vals_alt2, (size_t)n * 4) != hipSuccess ||
+            hipMalloc(&sc.hist11, (size_t)nb * kR11 * 4) != hipSuccess) {
+            err = "radix sort: out of device memory";
+            return GS_ERR_NOMEM;
+        }
+        sc.alt2_cap = (size_t)n;
+        sc.hist11_cap = (size_t)nb * kR11;
+    }
+    if (!sc.row11 && hipMalloc(&sc.row11, kR11 * 4) != hipSuccess) {
+        err = "radix sort: out of device memory";
+        return GS_ERR_NOMEM;
+    }
+    // keys -> alt -> alt2 -> keys
+    uint32_t *kin[3] = {keys, sc.keys_alt, sc.keys_alt2}, *vin[3] = {vals, sc.vals_alt, sc.vals_alt2};
+    uint32_t *kou[3] = {sc.keys_alt, sc.keys_alt2, keys}, *vou[3] = {sc.vals_alt, sc.vals_alt2, vals};
+    const int shifts[3] = {0, 11, 22};
+    for (int pass = 0; pass < 3; ++pass) {
+        hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 2 ? stop : nullptr;
+        const bool b10 = pass == 2;
+        const int R = b10 ? 1024 : 2048;
+        if (b10)
+            hipExtLaunchKernelGGL(k_upsweep11<10>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
+                                  (uint32_t)n, shifts[pass], sc.hist11, nb);
+        else
+            hipExtLaunchKernelGGL(k_upsweep11<11>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
+                                  (uint32_t)n, shifts[pass], sc.hist11, nb);
+        hipLaunchKernelGGL((k_scan_rows<64, false>), dim3(R), dim3(256), 0, s, sc.hist11, nb, (uint32_t)n, nullptr, kTile,
+                           sc.row11, nullptr, nullptr, PrefixDev{}, 0);
+        if (b10)
+            hipExtLaunchKernelGGL(k_downsweep11<10>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin[pass],
+                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, nb, sc.row11);
+        else
+            hipExtLaunchKernelGGL(k_downsweep11<11>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin[pass],
+                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, nb, sc.row11);
+    }
+    if (hipGetLastError() != hipSuccess) {
+        err = "radix sort: kernel launch failed";
+        return GS_ERR_HIP;
+    }
+    return GS_OK;
+}
+
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small) {
     // the most tiles of any pass (the small form keeps all four passes' histograms)
     // (small: the bucket pass's 1024-key tiles)
@@ -1495,6 +1695,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     }
     int rc = sort_ensure(sc, std::max<int64_t>(n, 1), err, s, small);
     if (rc) return rc;
+    if (GS_SORT11 && !pre && !bins && keys_out && !dev_count && dup_base < 0 && n >= (int64_t)1 << 24)
+        return sort_pairs11(s, sc, keys, vals, n, err, start, stop);
     uint32_t *tile_counts = sc.row_total + kRadix;
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
         if (start) (void)hipEventRecord(start, s);
