@@ -1414,15 +1414,22 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 // ---------------------------------------------------------------- GS_SORT11 (opt-in)
 // Standalone sorts of >= 16M pairs in three LSD passes of 11, 11 and 10 bits (VERDICT r4 item 5:
-// 4 + 3 x 16 bytes of pairs per key against 4 x 16 + 4), reduce-then-scan as the 8-bit passes:
-// k_upsweep11 (a 2048-bin histogram per 8192-key tile), k_scan_rows over the 2048 rows,
-// k_downsweep11 (stable ranking by an 11-bit match, the tile reordered in LDS, coalesced
-// scatter).  The per-wave digit counters and the reorder buffer share the LDS (positions are
-// kept in registers across the barrier): 80 KB, two workgroups per CU.
+// 4 + 3 x 16 bytes of pairs per key against 4 x 16 + 4), reduce-then-scan:
+//   k_upsweep11    a 2048-bin LDS histogram per 8192-key tile, stored tile-major (8 KB per tile,
+//                  one coalesced store);
+//   k_colscan11    per digit, the exclusive prefix over the tiles (in place) and the digit's total:
+//                  a workgroup per 8 digits, its 32 tile groups scanned then offset;
+//   k_downsweep11  sixteen waves of 8 keys per lane: stable ranking by an 11-bit ballot match,
+//                  per-wave 16-bit counters packed two to a word (64 KB, shared with the tile's
+//                  reorder buffer: positions stay in registers across the barrier), the tile's
+//                  2048 prefixes read contiguously, coalesced scatter.
 #ifndef GS_SORT11
 #define GS_SORT11 0
 #endif
 constexpr int kR11 = 2048;
+constexpr int kW11 = 16, kI11 = 8;                 // downsweep: waves, keys per lane
+constexpr int kT11 = kWaveBig * kWaveTile;         // 8192 keys per tile (= kW11 * 64 * kI11)
+static_assert(kW11 * 64 * kI11 == kT11, "one tile size for the three kernels");
 template <int BITS>
 __device__ __forceinline__ uint64_t match_digit_n(uint32_t d, uint64_t active) {
     uint32_t xlo = 0, xhi = 0;
@@ -1439,16 +1446,16 @@ __device__ __forceinline__ uint64_t match_digit_n(uint32_t d, uint64_t active) {
 
 template <int BITS>
 __global__ __launch_bounds__(kWaveBig * 64) void k_upsweep11(const uint32_t *__restrict__ keys, uint32_t n, int shift,
-                                                             uint32_t *__restrict__ hist, uint32_t nb) {
-    constexpr int kThreads = kWaveBig * 64, kTile = kThreads * kItems, R = 1 << BITS;
-    const uint32_t live = (n + kTile - 1) / kTile;
+                                                             uint32_t *__restrict__ hist) {
+    constexpr int kThreads = kWaveBig * 64, R = 1 << BITS;
+    const uint32_t live = (n + kT11 - 1) / kT11;
     const uint32_t tile = xcd_tile_rev(live);
     if (tile >= live) return;  // uniform
     __shared__ uint32_t s_cnt[R];
     for (int i = threadIdx.x; i < R; i += kThreads) s_cnt[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t base = tile * (uint32_t)kTile + wid * (uint32_t)kWaveTile + lane;
+    const uint32_t base = tile * (uint32_t)kT11 + wid * (uint32_t)kWaveTile + lane;
     uint32_t kk[kItems];
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
@@ -1459,39 +1466,66 @@ __global__ __launch_bounds__(kWaveBig * 64) void k_upsweep11(const uint32_t *__r
     for (int k = 0; k < kItems; ++k)
         if (base + k * 64 < n) atomicAdd(&s_cnt[(kk[k] >> shift) & (R - 1)], 1u);
     __syncthreads();
-    for (int d = threadIdx.x; d < R; d += kThreads) hist[(size_t)d * nb + tile] = s_cnt[d];
+    for (int d = threadIdx.x; d < R; d += kThreads) hist[(size_t)tile * R + d] = s_cnt[d];
+}
+
+// workgroup g: digits [8 g, 8 g + 8); thread (c = t / 8, d = t % 8) scans tiles [c * per, ...)
+template <int BITS>
+__global__ __launch_bounds__(256) void k_colscan11(uint32_t *__restrict__ hist, uint32_t nb, uint32_t *__restrict__ total) {
+    constexpr int R = 1 << BITS;
+    __shared__ uint32_t s_c[32][8];
+    const int t = threadIdx.x, c = t >> 3, dl = t & 7;
+    const uint32_t d = blockIdx.x * 8u + (uint32_t)dl;
+    const uint32_t per = (nb + 31) / 32, t0 = (uint32_t)c * per, t1 = min(nb, t0 + per);
+    uint32_t sum = 0;
+    for (uint32_t j = t0; j < t1; ++j) sum += hist[(size_t)j * R + d];
+    s_c[c][dl] = sum;
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+        const uint32_t v = s_c[q][dl];
+        off += q < c ? v : 0u;
+        tot += v;
+    }
+    for (uint32_t j = t0; j < t1; ++j) {
+        const uint32_t v = hist[(size_t)j * R + d];
+        hist[(size_t)j * R + d] = off;
+        off += v;
+    }
+    if (c == 0) total[d] = tot;
 }
 
 template <int BITS>
-__global__ __launch_bounds__(kWaveBig * 64) void k_downsweep11(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                               uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                               uint32_t n, int shift, const uint32_t *__restrict__ hist,
-                                                               uint32_t nb, const uint32_t *__restrict__ row_total) {
-    constexpr int W = kWaveBig, kThreads = W * 64, kTile = kThreads * kItems, R = 1 << BITS;
-    static_assert(W * kR11 * 4 >= kTile * 8, "the reorder buffer fits in the counters' LDS");
-    const uint32_t live = (n + kTile - 1) / kTile;
+__global__ __launch_bounds__(kW11 * 64) void k_downsweep11(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                            uint32_t n, int shift, const uint32_t *__restrict__ hist,
+                                                            const uint32_t *__restrict__ total) {
+    constexpr int W = kW11, kThreads = W * 64, R = 1 << BITS;
+    static_assert(W * (kR11 / 2) * 4 >= kT11 * 8, "the reorder buffer fits in the counters' LDS");
+    const uint32_t live = (n + kT11 - 1) / kT11;
     const uint32_t tile = xcd_tile(live);
     if (tile >= live) return;  // uniform
-    __shared__ uint32_t s_cnt[W][kR11];  // per-wave counters (R used), then the tile's keys and values
+    __shared__ uint32_t s_cnt[W][kR11 / 2];  // per-wave 16-bit counters, then the tile's keys and values
     __shared__ uint32_t s_start[R];
     __shared__ int32_t s_gbase[R];
     __shared__ uint32_t s_w[W];
-    uint32_t *s_keys = &s_cnt[0][0], *s_vals = &s_cnt[0][0] + kTile;
-    for (int i = threadIdx.x; i < W * kR11; i += kThreads) (&s_cnt[0][0])[i] = 0;
+    uint32_t *s_keys = &s_cnt[0][0], *s_vals = &s_cnt[0][0] + kT11;
+    for (int i = threadIdx.x; i < W * (kR11 / 2); i += kThreads) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t tile0 = tile * (uint32_t)kTile;
-    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems], vv[kItems];
+    const uint32_t tile0 = tile * (uint32_t)kT11;
+    const uint32_t base = tile0 + wid * (uint32_t)(64 * kI11) + lane;
+    uint32_t kk[kI11], vv[kI11];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < kI11; ++k) {
         const uint32_t idx = base + k * 64;
         kk[k] = idx < n ? kin[idx] : 0u;
         vv[k] = idx < n ? vin[idx] : 0u;
     }
-    uint32_t rank[kItems], lead[kItems], old[kItems];
+    uint32_t rank[kI11], lead[kI11], old[kI11];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < kI11; ++k) {
         const bool valid = base + k * 64 < n;
         const uint32_t d = (kk[k] >> shift) & (R - 1);
         const uint64_t m = match_digit_n<BITS>(d, __ballot(valid));
@@ -1499,60 +1533,85 @@ __global__ __launch_bounds__(kWaveBig * 64) void k_downsweep11(const uint32_t *_
         lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
         old[k] = valid ? (uint32_t)__popcll(m) : 0u;
     }
+    // (a wave holds at most 512 keys of a digit: 16-bit halves never carry)
 #pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if (base + k * 64 < n && lead[k] == (uint32_t)lane) old[k] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & (R - 1)], old[k]);
+    for (int k = 0; k < kI11; ++k)
+        if (base + k * 64 < n && lead[k] == (uint32_t)lane) {
+            const uint32_t d = (kk[k] >> shift) & (R - 1), sh = 16u * (d & 1u);
+            old[k] = (atomicAdd(&s_cnt[wid][d >> 1], old[k] << sh) >> sh) & 0xffffu;
+        }
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
+    for (int k = 0; k < kI11; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
     __syncthreads();
     // per digit: the waves' exclusive offsets, the tile's digit starts, the global bases
-    constexpr int DPT = R / kThreads;  // digits per thread (4 or 2)
-    uint32_t tot[DPT], a = 0;
+    constexpr int DPT = (R + kThreads - 1) / kThreads;  // digits per thread (2 or 1)
+    uint32_t tot[DPT], a = 0, g = 0;
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
         const int d = threadIdx.x * DPT + j;
         uint32_t t = 0;
+        if (d < R) {
+            const uint32_t sh = 16u * ((uint32_t)d & 1u);
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint32_t c = s_cnt[w][d];
-            s_cnt[w][d] = t;
-            t += c;
+            for (int w = 0; w < W; ++w) {
+                const uint32_t word = s_cnt[w][d >> 1];
+                const uint32_t c = (word >> sh) & 0xffffu;
+                // (the exclusive offset replaces the count in place; the other half is another
+                // thread's digit -- the pair belongs to one thread when DPT == 2)
+                s_cnt[w][d >> 1] = DPT == 2 ? (sh ? (word & 0xffffu) | (t << 16) : (word & 0xffff0000u) | t) : word;
+                t += c;
+            }
+            g += total[d];
         }
         tot[j] = t;
         a += t;
     }
-    const uint32_t ex = block_excl_scan<W>(a, s_w);
-    uint32_t g = 0;
+    if (DPT == 1) __syncthreads();  // (one digit per thread: the pair's halves are two threads')
+    if (DPT == 1) {
+        const int d = threadIdx.x;
+        // rewrite both halves of the pair from its even thread, the counts recomputed
+        if ((d & 1) == 0 && d + 1 < R) {
+            uint32_t t0 = 0, t1 = 0;
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) g += row_total[threadIdx.x * DPT + j];
+            for (int w = 0; w < W; ++w) {
+                const uint32_t word = s_cnt[w][d >> 1];
+                s_cnt[w][d >> 1] = (t0 & 0xffffu) | (t1 << 16);
+                t0 += word & 0xffffu;
+                t1 += word >> 16;
+            }
+        }
+    }
+    const uint32_t ex = block_excl_scan<W>(a, s_w);
     const uint32_t gex = block_excl_scan<W>(g, s_w);
     {
         uint32_t st = ex, gb = gex;
 #pragma unroll
         for (int j = 0; j < DPT; ++j) {
             const int d = threadIdx.x * DPT + j;
-            s_start[d] = st;
-            s_gbase[d] = (int32_t)(gb + hist[(size_t)d * nb + tile]) - (int32_t)st;
-            st += tot[j];
-            gb += row_total[d];
+            if (d < R) {
+                s_start[d] = st;
+                s_gbase[d] = (int32_t)(gb + hist[(size_t)tile * R + d]) - (int32_t)st;
+                st += tot[j];
+                gb += total[d];
+            }
         }
     }
     __syncthreads();
-    uint32_t pos[kItems];
+    uint32_t pos[kI11];
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t d = (kk[k] >> shift) & (R - 1);
-        pos[k] = s_start[d] + s_cnt[wid][d] + rank[k];
+    for (int k = 0; k < kI11; ++k) {
+        const uint32_t d = (kk[k] >> shift) & (R - 1), sh = 16u * (d & 1u);
+        pos[k] = s_start[d] + ((s_cnt[wid][d >> 1] >> sh) & 0xffffu) + rank[k];
     }
     __syncthreads();  // (the counters' LDS becomes the reorder buffer)
 #pragma unroll
-    for (int k = 0; k < kItems; ++k)
+    for (int k = 0; k < kI11; ++k)
         if (base + k * 64 < n) {
             s_keys[pos[k]] = kk[k];
             s_vals[pos[k]] = vv[k];
         }
     __syncthreads();
-    const uint32_t tile_n = min((uint32_t)kTile, n - tile0);
+    const uint32_t tile_n = min((uint32_t)kT11, n - tile0);
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
         const uint32_t o = (uint32_t)(s_gbase[(key >> shift) & (R - 1)] + (int32_t)i);
@@ -1563,8 +1622,7 @@ __global__ __launch_bounds__(kWaveBig * 64) void k_downsweep11(const uint32_t *_
 
 int sort_pairs11(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
                  hipEvent_t start, hipEvent_t stop) {
-    constexpr uint32_t kTile = kWaveBig * kWaveTile;
-    const uint32_t nb = (uint32_t)((n + kTile - 1) / kTile);
+    const uint32_t nb = (uint32_t)((n + kT11 - 1) / kT11);
     if ((size_t)n > sc.alt2_cap || (size_t)nb * kR11 > sc.hist11_cap) {
         (void)hipStreamSynchronize(s);
         for (uint32_t **p : {&sc.keys_alt2, &sc.vals_alt2, &sc.hist11})
@@ -1588,22 +1646,19 @@ int sort_pairs11(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals,
     const int shifts[3] = {0, 11, 22};
     for (int pass = 0; pass < 3; ++pass) {
         hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 2 ? stop : nullptr;
-        const bool b10 = pass == 2;
-        const int R = b10 ? 1024 : 2048;
-        if (b10)
+        if (pass == 2) {
             hipExtLaunchKernelGGL(k_upsweep11<10>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
-                                  (uint32_t)n, shifts[pass], sc.hist11, nb);
-        else
+                                  (uint32_t)n, shifts[pass], sc.hist11);
+            hipLaunchKernelGGL(k_colscan11<10>, dim3(1024 / 8), dim3(256), 0, s, sc.hist11, nb, sc.row11);
+            hipExtLaunchKernelGGL(k_downsweep11<10>, dim3(xcd_grid(nb)), dim3(kW11 * 64), 0, s, nullptr, e1, 0, kin[pass],
+                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, sc.row11);
+        } else {
             hipExtLaunchKernelGGL(k_upsweep11<11>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
-                                  (uint32_t)n, shifts[pass], sc.hist11, nb);
-        hipLaunchKernelGGL((k_scan_rows<64, false>), dim3(R), dim3(256), 0, s, sc.hist11, nb, (uint32_t)n, nullptr, kTile,
-                           sc.row11, nullptr, nullptr, PrefixDev{}, 0);
-        if (b10)
-            hipExtLaunchKernelGGL(k_downsweep11<10>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin[pass],
-                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, nb, sc.row11);
-        else
-            hipExtLaunchKernelGGL(k_downsweep11<11>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0, kin[pass],
-                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, nb, sc.row11);
+                                  (uint32_t)n, shifts[pass], sc.hist11);
+            hipLaunchKernelGGL(k_colscan11<11>, dim3(2048 / 8), dim3(256), 0, s, sc.hist11, nb, sc.row11);
+            hipExtLaunchKernelGGL(k_downsweep11<11>, dim3(xcd_grid(nb)), dim3(kW11 * 64), 0, s, nullptr, e1, 0, kin[pass],
+                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, sc.row11);
+        }
     }
     if (hipGetLastError() != hipSuccess) {
         err = "radix sort: kernel launch failed";
