@@ -40,6 +40,12 @@ constexpr int kTileSmall = kWaveSmall * kWaveTile;  // 4096
 #define GS_PREFIX_P0_WAVES GS_WAVE_BIG
 #endif
 constexpr int kP0Waves = GS_PREFIX_P0_WAVES;
+// keys per lane in a prefix sort's passes 1-3 (the ~1M kept keys of a frame: 8 -> 2048-key tiles, twice
+// the workgroups of the 4096-key form; same box: sort stage 0.132 -> 0.123 ms, one frame -1 %)
+#ifndef GS_SUB_ITEMS
+#define GS_SUB_ITEMS 8
+#endif
+constexpr int kSubItems = GS_SUB_ITEMS;
 constexpr int kRadix = 256;
 constexpr int kRep = 8;  // upsweep counter replicas per digit (lane % 8)
 
@@ -540,14 +546,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 
 // PREFIX: the first pass of a prefix sort -- only the keys at or below their class bound move
 // BKT: the digit is the key's bucket (bucket_of: its tile class) -- the scatter of the class sort
 constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2, kPlace = 3;
-template <int W, int FMT, bool PREFIX = false, bool BKT = false>
+template <int W, int FMT, bool PREFIX = false, bool BKT = false, int IT = kItems>
 __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
                                                       const uint32_t *__restrict__ hist, uint32_t nb,
                                                       const uint32_t *__restrict__ row_total, PrefixDev pre,
                                                       uint32_t dup_base) {
-    constexpr int kThreads = W * 64, kTile = kThreads * kItems, kWaves = W;
+    constexpr int kThreads = W * 64, kTile = kThreads * IT, kWaves = W, kWT = 64 * IT;
     static_assert(kThreads >= kRadix, "one thread per digit scans the counts");
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
@@ -569,12 +575,12 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     __syncthreads();
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     const uint32_t tile0 = tile * (uint32_t)kTile;
-    const uint32_t base = tile0 + wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems], vv[kItems];
+    const uint32_t base = tile0 + wid * (uint32_t)kWT + lane;
+    uint32_t kk[IT], vv[IT];
     if (dup_base != kNoSplit) {  // uniform: the split emission layout (see k_upsweep)
         const uint32_t v0 = cnt[0], gap = dup_base - v0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t idx = base + k * 64;
             const uint32_t a = split_at(idx, v0, gap);
             kk[k] = (idx < n) ? kin[a] : 0u;
@@ -583,13 +589,13 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     } else if (tile0 + kTile <= n) {  // uniform: full tile, immediate offsets
         const uint32_t *pk = kin + base, *pv = vin + base;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             kk[k] = pk[k * 64];
             vv[k] = FMT == kPackIn ? 0u : pv[k * 64];
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t idx = base + k * 64;
             kk[k] = (idx < n) ? kin[idx] : 0u;
             vv[k] = (FMT != kPackIn && idx < n) ? vin[idx] : 0u;
@@ -602,17 +608,17 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     //      returned value is the count of that digit in the earlier items; all 16 atomics are
     //      issued back to back (one LDS round trip, not one per item);
     //   3. peers fetch their leader's returned value (ds_bpermute).
-    uint32_t rank[kItems], lead[kItems], old[kItems];
+    uint32_t rank[IT], lead[IT], old[IT];
     uint32_t keepm = 0;  // PREFIX: bit k = item k is kept (after the compaction: k * 64 + lane < kept)
-    uint32_t nit = kItems;  // items holding elements (uniform)
+    uint32_t nit = IT;  // items holding elements (uniform)
     if (PREFIX) {
         // The kept keys of the wave (about a fifth) move to the front of its 1024 slots, in
         // (item, lane) order -- the order stability needs -- so only ceil(kept / 64) items are
         // ranked.  (s_keys / s_vals are free until the block-level reorder below.)
-        uint32_t *ck = s_keys + wid * kWaveTile, *cv = s_vals + wid * kWaveTile;
+        uint32_t *ck = s_keys + wid * kWT, *cv = s_vals + wid * kWT;
         uint32_t nk = 0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const bool keep = base + k * 64 < n && kk[k] <= (uint32_t)s_cls[key_class(kk[k])];
             const uint64_t m = __ballot(keep);
             if (keep) {
@@ -627,7 +633,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         nit = (nk + 63) / 64;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
+        for (int k = 0; k < IT; ++k) {
             const uint32_t slot = (uint32_t)(k * 64 + lane);
             if ((uint32_t)k < nit && slot < nk) {
                 kk[k] = ck[slot];
@@ -657,10 +663,10 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         _Pragma("unroll") for (int k = 0; k < (NI); ++k) rank[k] +=                                   \
             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);                 \
     } while (0)
-    if (!PREFIX) GS_RANK_ITEMS(kItems);
-    else if (nit <= kItems / 4) GS_RANK_ITEMS(kItems / 4);  // uniform
-    else if (nit <= kItems / 2) GS_RANK_ITEMS(kItems / 2);
-    else GS_RANK_ITEMS(kItems);
+    if (!PREFIX) GS_RANK_ITEMS(IT);
+    else if (nit <= IT / 4) GS_RANK_ITEMS(IT / 4);  // uniform
+    else if (nit <= IT / 2) GS_RANK_ITEMS(IT / 2);
+    else GS_RANK_ITEMS(IT);
 #undef GS_RANK_ITEMS
     __syncthreads();
     {
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const uint32_t idx = base + k * 64;
         const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
         if (valid) {
@@ -1670,7 +1676,8 @@ int sort_pairs11(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals,
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small) {
     // the most tiles of any pass (the small form keeps all four passes' histograms)
     // (small: the bucket pass's 1024-key tiles)
-    const size_t tsz = small ? kTileSmall / 4 : kTileSmall;
+    // (and a prefix sort's passes 1-3: kSubItems keys per lane)
+    const size_t tsz = small ? kTileSmall / 4 : std::min(kTileSmall, kWaveSmall * 64 * kSubItems);
     const size_t nb = (size_t)((n + tsz - 1) / tsz) + 3;  // (+3: the small form's 16-byte rows)
     const bool grow_alt = (size_t)n > sc.alt_cap, grow_hist = nb * kRadix > sc.hist_cap;
     if ((grow_alt && sc.keys_alt) || (grow_hist && sc.hist)) (void)hipStreamSynchronize(s);  // in-flight users
@@ -1864,7 +1871,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         const bool big = (pass == 0 && !kept_in) || all_big;
         // (a prefix sort's first pass keeps ~1 key in 8: its tiles of kP0Waves waves)
         const bool p0 = big && pre && !kept_in;
-        const uint32_t tile = p0 ? kP0Waves * kWaveTile : big ? kWaveBig * kWaveTile : kTileSmall;
+        // (a prefix sort's passes on the kept keys: kSubItems keys per lane)
+        const bool sub = pre && !big;
+        const uint32_t tile = p0 ? kP0Waves * kWaveTile : big ? kWaveBig * kWaveTile : sub ? kWaveSmall * 64 * kSubItems : kTileSmall;
         // a prefix sort's passes 1-3 run on the kept keys (their count on the device, at most n_sub)
         const uint32_t *cnt = pre && pass > 0 ? pre->nsel : kept_in ? kept->count : dev_count;
         const int64_t np = pass > 0 || kept_in ? n_sub : n;
@@ -1885,6 +1894,9 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         else if (big)
             hipExtLaunchKernelGGL((k_upsweep<kWaveBig, false>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0,
                                   kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, split);
+        else if (sub)
+            hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false, false, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64),
+                                  0, s, e0, nullptr, 0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, kNoSplit);
         else
             hipExtLaunchKernelGGL((k_upsweep<kWaveSmall, false>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, e0, nullptr,
                                   0, kin, (uint32_t)np, cnt, shift, sc.hist, nb, nullptr, pd, kNoSplit);
@@ -1917,6 +1929,12 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
         else if (big)
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
                                   kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
+        else if (sub && fmt == kPairs)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs, false, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
+                                  s, nullptr, e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
+        else if (sub && fmt == kPlace)
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace, false, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
+                                  s, nullptr, e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (fmt == kPairs)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
                                   0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
