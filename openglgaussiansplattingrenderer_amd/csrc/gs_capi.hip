@@ -95,6 +95,7 @@ struct Lane {
     int64_t e_cap = 0;
     uint32_t *keys = nullptr, *vals = nullptr;
     uint32_t *vals_base = nullptr;  // the allocation: kValsPad zero words, then vals (k_draw reads vals[-1] = 0)
+    uint2 *sbox_base = nullptr;     // GS_DRAW_SBOX: one empty box, then the boxes by position
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     bool vals_partial = false;  // the frame was prefix-sorted: vals holds only each list's sorted prefix
     uint32_t *pre_buf = nullptr;  // prefix-sort state (gs::kPrefixWords words, see gs::PrefixDev)
@@ -360,6 +361,10 @@ int ensure_entries(gs_ctx *ctx, int64_t e) {
     // the rest is zeroed too, so every word a kernel could read before it is written is a valid id
     GS_HIP(ctx, hipMemsetAsync(ctx->L->vals_base, 0, ((size_t)cap + gs::kValsPad) * 4, ctx->L->stream));
     GS_HIP(ctx, hipMemsetAsync(ctx->L->keys, 0, (size_t)cap * 4, ctx->L->stream));
+    if (GS_DRAW_SBOX) {  // all ones: every box empty (the one before position 0 stays so)
+        if ((rc = grow(ctx, ctx->L->sbox_base, (size_t)cap + 1))) return rc;
+        GS_HIP(ctx, hipMemsetAsync(ctx->L->sbox_base, 0xff, ((size_t)cap + 1) * 8, ctx->L->stream));
+    }
     ctx->L->vals = ctx->L->vals_base + gs::kValsPad;
     ctx->L->e_cap = cap;
     return GS_OK;
@@ -682,7 +687,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
         void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
-                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb, ln.kdup, ln.blocksum_k};
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb, ln.kdup, ln.blocksum_k, ln.sbox_base};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
@@ -1224,6 +1229,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.V = (int32_t)ctx->V;  // used when count is null (the frame's counts are on the host)
     P.prefix = prefix ? 1 : 0;
     P.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;  // (every blend of the context refreshes the per-tile depths)
+    P.sbox = (GS_DRAW_SBOX && prefix && !gs::kPrefixClassSort) ? ctx->L->sbox_base + 1 : nullptr;  // (the class sort places no boxes)
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other
@@ -1327,6 +1333,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.cap_sel = cap_for(sel_turned);
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
+
     }
     const bool fused = gs::preprocess_blocks(scene->n) <= kFusedMaxBlocks;
     // GS_FLAG_SH with the prefix sort: colour only the kept entries' splats, after the sort
@@ -1421,6 +1428,9 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         if (ctx->theta_ev_live) GS_HIP(ctx, hipStreamWaitEvent(ctx->L->stream, ctx->theta_ev, 0));
         ks.count = nullptr;
     }
+    // (the lane's cull boxes exist once its preprocess was enqueued: a fresh lane allocates them there)
+    pd.cullbox = ctx->L->cullbox;
+    pd.box_out = GS_DRAW_SBOX ? ctx->L->sbox_base + 1 : nullptr;
     if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
                            ctx->E < ctx->small_sort_entries, kept_base ? &ks : nullptr)))
         return rc;

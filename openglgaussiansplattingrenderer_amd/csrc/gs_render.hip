@@ -1715,6 +1715,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // memory latency per step.
     constexpr uint32_t kBatch = GS_DRAW_BATCH;
     uint32_t Vi[2], Vb[2];      // indices: as loaded / riding with the box gather
+    uint32_t Oi[2];             // GS_DRAW_SBOX: the index's word offset from vals - 1 (its box's too)
     uint2 Bx[2];                // boxes (int16 pixel bounds, pack_box)
     SurvData Dd;                // the batch's survivor data (lane j: survivor j)
     SurvRgb Dc;                 // ... colour
@@ -1732,17 +1733,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     };
     // position p -> word of vals - 1 (the word before vals is 0: a culled entry, splat 0)
     const uint32_t *vals_m1 = vals - 1;
-    auto load_idx = [&](int base, uint32_t &v) {
+    auto load_idx = [&](int base, uint32_t &v, uint32_t &off) {
         const int p = min(base + lane, jmax);
         const int q = p < cpos ? p : p < cpos + cn ? -1 : p - cn;
-        v = *at(vals_m1, (uint32_t)(min(q, qmax) + 1) << 2);
+        off = (uint32_t)(min(q, qmax) + 1);
+        v = *at(vals_m1, off << 2);
     };
     // (ids clamped to the scene: the gathers stay inside the per-splat buffers whatever a frame's
     // values hold -- the clamp sits here, where the index load has arrived, not at the load)
     const uint32_t idmax = (uint32_t)max(P.n - 1, 0);
-    auto gather_box = [&](uint32_t v, uint32_t &vb, uint2 &bx) {
+    // (GS_DRAW_SBOX, a prefix-sorted frame: the box at the entry's position, read in list order;
+    // one load either way -- the base and offset are selected, not the load)
+    const bool sorted_box = GS_DRAW_SBOX && P.sbox != nullptr;
+    const uint2 *box_base = sorted_box ? P.sbox - 1 : cullbox;
+    auto gather_box = [&](uint32_t v, uint32_t off, uint32_t &vb, uint2 &bx) {
         vb = min(v, idmax);
-        bx = *at(cullbox, vb << 3);
+        bx = *at(box_base, (sorted_box ? off : vb) << 3);
     };
     // box test of a chunk; its survivors join the queue
     auto test_and_queue = [&](int cbase, uint32_t v, const uint2 &bx) __attribute__((always_inline)) {
@@ -2027,17 +2033,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // prologue: chunk 0 index-loaded and box-gathered, chunk 1 index-loaded
     int base = start;
     if (base < end && !all_done) {  // uniform
-        uint32_t v0;
-        load_idx(base, v0);
-        load_idx(base + 64, Vi[1]);
-        gather_box(v0, Vb[0], Bx[0]);
+        uint32_t v0, o0;
+        load_idx(base, v0, o0);
+        load_idx(base + 64, Vi[1], Oi[1]);
+        gather_box(v0, o0, Vb[0], Bx[0]);
         // chunk c's stages use slot c & 1 for the box and (c + 1) & 1 for the next index; step c
         // (slot u = c & 1) issues the loads of chunks c+1..c+2, tests chunk c, then blends the
         // batch in flight and issues the next one
         auto step = [&](auto U) {
             constexpr int u = decltype(U)::value, w = u ^ 1;
-            load_idx(base + 128, Vi[u]);       // chunk c+2
-            gather_box(Vi[w], Vb[w], Bx[w]);   // chunk c+1
+            load_idx(base + 128, Vi[u], Oi[u]);        // chunk c+2
+            gather_box(Vi[w], Oi[w], Vb[w], Bx[w]);    // chunk c+1
             test_and_queue(base, Vb[u], Bx[u]);  // chunk c
             if (STATS) ++st_iter;
             if (inflight) blend_batch();

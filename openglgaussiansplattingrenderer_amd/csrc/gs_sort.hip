@@ -704,6 +704,29 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     }
     __syncthreads();
     const uint32_t tile_n = PREFIX ? s_tile_n : min((uint32_t)kTile, n - tile0);
+    if (FMT == kPlace && GS_DRAW_SBOX && pre.box_out) {  // uniform
+        // the placed values' cull boxes too (GS_DRAW_SBOX): every item's box gather in flight
+        // before any is stored (a gather per loop trip waited one memory latency each)
+        uint2 bx[IT];
+        uint32_t at[IT];
+        const uint32_t idmax = (uint32_t)max(pre.n - 1, 0);
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            const uint32_t i = threadIdx.x + (uint32_t)(k * kThreads);
+            const bool ok = i < tile_n;
+            const uint32_t ii = ok ? i : 0u;
+            const uint32_t key = s_keys[ii];
+            const uint32_t o = (uint32_t)(s_gbase[digit_of<BKT>(key, shift)] + (int32_t)ii);
+            const uint32_t id = s_vals[ii];
+            at[k] = ok ? (uint32_t)((int32_t)o + s_cls[key_class(key)]) : 0xffffffffu;
+            bx[k] = pre.cullbox[min(id, idmax)];
+            if (ok) vout[at[k]] = id;
+        }
+#pragma unroll
+        for (int k = 0; k < IT; ++k)
+            if (at[k] != 0xffffffffu) pre.box_out[at[k]] = bx[k];
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
         const uint32_t d = digit_of<BKT>(key, shift);
