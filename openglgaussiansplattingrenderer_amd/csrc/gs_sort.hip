@@ -558,6 +558,11 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     const uint32_t n = elem_count(n_max, cnt);
     const uint32_t live = (n + kTile - 1) / kTile;
     const uint32_t tile = xcd_tile(live);
+    // GS_DRAW_SBOX: the box before position 0 is what k_draw reads for the reference's culled
+    // entries (a Q10 window past the last tile list; drawn as splat 0, preprocess.glsl:80-88,
+    // draw.glsl:97-98): splat 0's box of this frame (its culled record when it has no entries)
+    if (FMT == kPlace && GS_DRAW_SBOX && pre.box_out && blockIdx.x == 0 && threadIdx.x == 0)
+        pre.box_out[-1] = pre.cullbox[0];
     if (tile >= live) return;  // uniform: tile beyond the count
     __shared__ uint32_t s_cnt[kWaves][kRadix];  // running per-wave counts -> per-wave exclusive offsets
     __shared__ uint32_t s_start[kRadix];        // block-local start of each digit

@@ -165,6 +165,52 @@ def test_prefix_misses_render_again():
     ctx.close()
 
 
+def test_prefix_sorted_boxes_draw_culled_entries_as_splat_zero(oracle):
+    """VERDICT r5 / ADVICE r5 (medium): on a prefix-sorted frame the blend reads each entry's cull
+    box in sorted order (GS_DRAW_SBOX).  The last tile's Q10 window runs past its list into the
+    reference's culled entries, drawn as splat 0 (preprocess.glsl:80-88, draw.glsl:97-98); their
+    box is splat 0's.  Scene (tests/culled_scene.py, n_bulk): millions of entries in the low tiles
+    (the prefix sort engages), splat 0 visible in tile 255 with a list far shorter than the target
+    and not a multiple of 1024, 300 culled splats, no key in [256, 1e6) -- so no prefix limit stops
+    the window.  The prefix-sorted frames must equal the oracle and the full sort bit for bit."""
+    from tests.culled_scene import culled_scene
+    W, H = 1024, 512
+    ctx = g.Context(0)
+    means, col, op, log_sc, rot, u = culled_scene(g, W, H, n_bulk=30_000)
+    sp = g.Splats.from_raw(means, col, op, log_sc, rot, W, H, ctx=ctx)
+    o = oracle.render(sp.means3D, sp.covarianceMatrices, sp.opacities, sp.colours, u, flags=0, draw=True)
+    assert sp.numSplats - o["V"] == 300
+    keys = o["keys"].view(np.float32)
+    assert not np.any((keys >= 256.0) & (keys < 1.0e6))
+    bins = o["bins"].astype(np.int64)
+    n255 = int(bins[255] - bins[254])
+    assert 0 < n255 < 4096 and n255 % 1024 != 0, n255
+    # the culled entries matter: the oracle's blend without them differs in the last row of tiles
+    O = oracle
+    img_no = np.zeros_like(o["image"])
+    O.lib().ora_draw(W, H, 0, O._p(o["bins"]), O._p(o["vals"]), o["E"], O._p(o["means2d"]), O._p(o["conics"]),
+                     O._p(np.ascontiguousarray(sp.colours, np.float32)), O._p(img_no))
+    diff = np.any(img_no != o["image"], axis=2)
+    assert diff[15 * H // 16:, 15 * W // 16:].sum() > 50 and not diff[: 15 * H // 16].any()
+    ref = g.DeviceBuffer(ctx, W * H * 4)
+    st = render_sync(sp, u, ref)
+    assert st.entries >= 64 * 32768, st.entries
+    img_full = ref.download(np.uint8, W * H * 4)
+    assert np.array_equal(img_full.reshape(H, W, 4), o["image"])
+    assert ctx.set_sort_prefix() == 32768
+    ctx.prefix_stats(reset=True)
+    outs = [g.DeviceBuffer(ctx, W * H * 4) for _ in range(3)]
+    for k in range(3):
+        render_spec(sp, u, outs[k])
+    ctx.sync()
+    ps = ctx.prefix_stats()
+    assert ps["frames"] == 3 and ps["redone"] == 0, ps
+    assert ps["kept"] < ps["entries"], ps
+    for k in range(3):
+        assert np.array_equal(outs[k].download(np.uint8, W * H * 4), img_full), f"frame {k}"
+    ctx.close()
+
+
 def test_prefix_off_and_stage_calls():
     """target 0 turns the prefix sort off; after a prefix-sorted frame the stage API (a draw of
     the frame's lists, a re-sort) sees the whole sorted lists."""
