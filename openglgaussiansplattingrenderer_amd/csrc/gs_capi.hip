@@ -95,7 +95,8 @@ struct Lane {
     int64_t e_cap = 0;
     uint32_t *keys = nullptr, *vals = nullptr;
     uint32_t *vals_base = nullptr;  // the allocation: kValsPad zero words, then vals (k_draw reads vals[-1] = 0)
-    uint2 *sbox_base = nullptr;     // GS_DRAW_SBOX: one empty box, then the boxes by position
+    uint2 *sbox_base = nullptr;     // GS_DRAW_SBOX: splat 0's box, then the boxes by position
+    int64_t sbox_cap = 0;           // ... positions it holds (allocated by the first prefix-sorted frame)
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     bool vals_partial = false;  // the frame was prefix-sorted: vals holds only each list's sorted prefix
     uint32_t *pre_buf = nullptr;  // prefix-sort state (gs::kPrefixWords words, see gs::PrefixDev)
@@ -224,11 +225,12 @@ struct gs_ctx {
     // the class bounds the frame before it selected.  Two bound buffers: frame k reads
     // theta_buf[theta_cur] (its preprocess counts, its emission writes) and its select writes the
     // other one for frame k + 1, whose preprocess waits (on the device) for theta_ev, recorded
-    // behind that select.  Each buffer holds two bound sets: [0, kClasses) with the tiles' own
-    // depths, [kClasses, 2 kClasses) with their neighbourhoods' (for a frame k + 1 that turned
-    // since frame k: its content moved by a fraction of a tile).  theta_valid: the read buffer
-    // holds a select's bounds of this scene (else it is reset to "keep every entry", and that
-    // frame sorts all of them).
+    // behind that select.  Each buffer holds one bound set of kClasses words, selected with the
+    // tiles' own depths or -- by a frame that turned since the one before (PrefixDev::use_depth
+    // 0) -- with their 3x3 neighbourhoods' deepest; a turned frame emits every entry itself, and
+    // the set it selects is the one the next unturned frame keeps by.  theta_valid: the read
+    // buffer holds a select's bounds of this scene (else it is reset to "keep every entry", and
+    // that frame sorts all of them).
     uint32_t *theta_buf[2] = {nullptr, nullptr};
     int theta_cur = 0;
     hipEvent_t theta_ev = nullptr;
@@ -361,10 +363,6 @@ int ensure_entries(gs_ctx *ctx, int64_t e) {
     // the rest is zeroed too, so every word a kernel could read before it is written is a valid id
     GS_HIP(ctx, hipMemsetAsync(ctx->L->vals_base, 0, ((size_t)cap + gs::kValsPad) * 4, ctx->L->stream));
     GS_HIP(ctx, hipMemsetAsync(ctx->L->keys, 0, (size_t)cap * 4, ctx->L->stream));
-    if (GS_DRAW_SBOX) {  // all ones: every box empty (the one before position 0 stays so)
-        if ((rc = grow(ctx, ctx->L->sbox_base, (size_t)cap + 1))) return rc;
-        GS_HIP(ctx, hipMemsetAsync(ctx->L->sbox_base, 0xff, ((size_t)cap + 1) * 8, ctx->L->stream));
-    }
     ctx->L->vals = ctx->L->vals_base + gs::kValsPad;
     ctx->L->e_cap = cap;
     return GS_OK;
@@ -1229,7 +1227,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.V = (int32_t)ctx->V;  // used when count is null (the frame's counts are on the host)
     P.prefix = prefix ? 1 : 0;
     P.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;  // (every blend of the context refreshes the per-tile depths)
-    P.sbox = (GS_DRAW_SBOX && prefix && !gs::kPrefixClassSort) ? ctx->L->sbox_base + 1 : nullptr;  // (the class sort places no boxes)
+    P.sbox = (GS_DRAW_SBOX && prefix) ? ctx->L->sbox_base + 1 : nullptr;
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other
@@ -1294,15 +1292,14 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     gs::PrefixDev pd{};
     // passes 1-3 sized for the kept count of the newest retired prefix-sorted frame of the same
     // selection (with / without the depths) + 25 % (+ 64Ki); else every entry.  (Scaled by the
-    // depth since: a miss doubles it, and the kept count roughly with it; the class sort holds any
-    // kept count: no passes sized from an earlier frame.)
+    // depth since: a miss doubles it, and the kept count roughly with it.)
     auto cap_for = [&](bool turned_sel) -> uint32_t {
         const int64_t cap_e = ctx->L->e_cap;
         const int64_t kept = ctx->prefix_kept_target > 0 && ctx->prefix_target > ctx->prefix_kept_target
                                  ? (int64_t)ctx->prefix_kept * ctx->prefix_target / ctx->prefix_kept_target
                                  : (int64_t)ctx->prefix_kept;
         const bool same_sel = ctx->prefix_kept_turned == turned_sel;
-        return (uint32_t)(!gs::kPrefixClassSort && ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
+        return (uint32_t)(ctx->prefix_kept && same_sel && !ctx->prefix_after_miss
                               ? std::min<int64_t>(cap_e, kept * 5 / 4 + 65536)
                               : cap_e);
     };
@@ -1333,7 +1330,13 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         pd.cap_sel = cap_for(sel_turned);
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
-
+        // GS_DRAW_SBOX: the cull boxes by sorted position, one per entry (only prefix-sorted frames
+        // use them: allocated here, not with the entries; all ones = empty boxes until placed)
+        if (GS_DRAW_SBOX && ctx->L->sbox_cap < ctx->L->e_cap) {
+            if (int rc = grow(ctx, ctx->L->sbox_base, (size_t)ctx->L->e_cap + 1)) return rc;
+            GS_HIP(ctx, hipMemsetAsync(ctx->L->sbox_base, 0xff, ((size_t)ctx->L->e_cap + 1) * 8, ctx->L->stream));
+            ctx->L->sbox_cap = ctx->L->e_cap;
+        }
     }
     const bool fused = gs::preprocess_blocks(scene->n) <= kFusedMaxBlocks;
     // GS_FLAG_SH with the prefix sort: colour only the kept entries' splats, after the sort
@@ -1343,7 +1346,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     // bounds the frame before it selected.  A turned frame emits every entry and selects its own
     // (its content moved: bounds selected at the other pose missed, tests/test_gpu_prefix.py);
     // either kind's select writes the bounds the next frame keeps by.
-    const bool kept_base = prefix && !fused && ctx->kept_emit && !gs::kPrefixClassSort && !lazy_loads(ctx, scene->n);
+    const bool kept_base = prefix && !fused && ctx->kept_emit && !lazy_loads(ctx, scene->n);
     const bool kept_mode = kept_base && !sel_turned;
     const uint32_t *theta_in = nullptr;
     if (kept_base) {
@@ -1430,7 +1433,7 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
     }
     // (the lane's cull boxes exist once its preprocess was enqueued: a fresh lane allocates them there)
     pd.cullbox = ctx->L->cullbox;
-    pd.box_out = GS_DRAW_SBOX ? ctx->L->sbox_base + 1 : nullptr;
+    pd.box_out = GS_DRAW_SBOX && prefix ? ctx->L->sbox_base + 1 : nullptr;
     if ((rc = enqueue_sort(ctx, ctx->L->e_cap, cnt, true, prefix ? &pd : nullptr, fused ? scene->n : -1,
                            ctx->E < ctx->small_sort_entries, kept_base ? &ks : nullptr)))
         return rc;

@@ -69,15 +69,6 @@ constexpr int kBinCountWords = 260;  // counts of k_bins_count: [0, 256) tiles, 
 //     that was not sorted (bins[kBinsLimit + t]); a sub-block that reaches it unsaturated flags
 //     the frame (pinned ring word 2 = 1), which is then rendered again with the full sort.
 constexpr int kClasses = 257;
-// the prefix sort's form: 0 (default) -- the kept subset through three more 8-bit LSD passes
-// (13 launches), sized for the previous frame's kept count (cap_sel); 1 -- one pass scatters the
-// kept keys by tile class and one launch sorts each class in LDS (gs_sort.hip k_class_sort, 5
-// launches; bit-exact, but slower at C3 so far: classes over 16k kept keys take a global-memory
-// path)
-#ifndef GS_CLASS_SORT
-#define GS_CLASS_SORT 0
-#endif
-constexpr bool kPrefixClassSort = GS_CLASS_SORT != 0;
 constexpr int kPrefixBuckets = 2048;
 constexpr int kPrefixSample = 128;
 constexpr int kPrefixHistCopies = 2;
@@ -203,13 +194,6 @@ struct SortScratch {
     size_t hist_cap = 0;           // elements
     uint32_t *row_total = nullptr; // [256], then [16][256] tile counts (zero between sorts)
     uint32_t *bkt = nullptr;       // [2][256]: the bucket form's bucket bases and counts
-    uint32_t *vals_scr = nullptr;  // the prefix class sort's scratch values (long buckets)
-    size_t scr_cap = 0;
-    // GS_SORT11 (standalone sorts of >= 16M pairs in three passes of 11/11/10-bit digits): the
-    // [2048][nb] histograms, the row totals, and a second alternate pair array (three passes:
-    // keys -> alt -> alt2 -> keys)
-    uint32_t *hist11 = nullptr, *row11 = nullptr, *keys_alt2 = nullptr, *vals_alt2 = nullptr;
-    size_t hist11_cap = 0, alt2_cap = 0;
 };
 
 // Stable sort of (key, value) pairs: n elements, or -- when dev_count is given -- min(n,

@@ -476,10 +476,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 
         __shared__ __attribute__((aligned(16))) uint32_t s_PG[2 * (kClasses + 1) + 1];
         if (prefix == 1) {
             prefix_counts(tile_counts, pre, cnt, n_max, s_w);
-        } else if (prefix == 3) {  // the class sort's single pass: the class tables, then the draw limits
-            prefix_counts(tile_counts, pre, cnt, n_max, s_w);
-            __syncthreads();  // (workgroup scope: this workgroup's class-table stores before its reads)
-            prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w, s_PG);
         } else if (prefix == 2) {
             prefix_limits(tile_counts, bins, pre, pre.frame_count, s_w, s_PG);
         } else {
@@ -544,9 +540,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPer <= 16 
 //   kPlace   (key, value) in, value out at its position in the full order: the last pass of a
 //            frame's prefix sort (position in the subset + pre.delta[class of the key])
 // PREFIX: the first pass of a prefix sort -- only the keys at or below their class bound move
-// BKT: the digit is the key's bucket (bucket_of: its tile class) -- the scatter of the class sort
 constexpr int kPairs = 0, kPackOut = 1, kPackIn = 2, kPlace = 3;
-template <int W, int FMT, bool PREFIX = false, bool BKT = false, int IT = kItems>
+template <int W, int FMT, bool PREFIX = false, int IT = kItems>
 __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                       uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                       uint32_t n_max, const uint32_t *__restrict__ cnt, int shift,
@@ -653,7 +648,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         _Pragma("unroll") for (int k = 0; k < (NI); ++k) {                                            \
             const uint32_t idx = base + k * 64;                                                       \
             const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
-            const uint32_t d = digit_of<BKT>(kk[k], shift);                                           \
+            const uint32_t d = digit_of<false>(kk[k], shift);                                           \
             const uint64_t m = match_digit(d, __ballot(valid));                                       \
             rank[k] = count_below(m);                                                                 \
             lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;                          \
@@ -663,7 +658,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
             const uint32_t idx = base + k * 64;                                                       \
             const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;                           \
             if (valid && lead[k] == (uint32_t)lane)                                                   \
-                old[k] = atomicAdd(&s_cnt[wid][digit_of<BKT>(kk[k], shift)], old[k]);                 \
+                old[k] = atomicAdd(&s_cnt[wid][digit_of<false>(kk[k], shift)], old[k]);                 \
         }                                                                                             \
         _Pragma("unroll") for (int k = 0; k < (NI); ++k) rank[k] +=                                   \
             (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);                 \
@@ -701,7 +696,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
         const uint32_t idx = base + k * 64;
         const bool valid = PREFIX ? ((keepm >> k) & 1u) != 0 : idx < n;
         if (valid) {
-            const uint32_t d = digit_of<BKT>(kk[k], shift);
+            const uint32_t d = digit_of<false>(kk[k], shift);
             const uint32_t pos = s_start[d] + s_cnt[wid][d] + rank[k];
             s_keys[pos] = kk[k];
             if (FMT != kPackIn) s_vals[pos] = vv[k];
@@ -721,7 +716,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
             const bool ok = i < tile_n;
             const uint32_t ii = ok ? i : 0u;
             const uint32_t key = s_keys[ii];
-            const uint32_t o = (uint32_t)(s_gbase[digit_of<BKT>(key, shift)] + (int32_t)ii);
+            const uint32_t o = (uint32_t)(s_gbase[digit_of<false>(key, shift)] + (int32_t)ii);
             const uint32_t id = s_vals[ii];
             at[k] = ok ? (uint32_t)((int32_t)o + s_cls[key_class(key)]) : 0xffffffffu;
             bx[k] = pre.cullbox[min(id, idmax)];
@@ -734,7 +729,7 @@ __global__ __launch_bounds__(W * 64) void k_downsweep(const uint32_t *__restrict
     }
     for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
         const uint32_t key = s_keys[i];
-        const uint32_t d = digit_of<BKT>(key, shift);
+        const uint32_t d = digit_of<false>(key, shift);
         const uint32_t o = (uint32_t)(s_gbase[d] + (int32_t)i);
         if (FMT == kPairs) {
             kout[o] = key;
@@ -1116,243 +1111,6 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
         }
 }
 
-// ------------------------------------------------------ the prefix sort's class sort
-// A frame's prefix sort (PrefixDev) keeps, per tile class, the keys at or below the class bound --
-// each class's kept keys a prefix of its sorted list, ~1.2M of C3's 10M entries.  Instead of three
-// more 8-bit LSD passes over the kept subset (9 launches), the first pass scatters the kept keys by
-// their bucket (bucket_of: the tile class; classes 255 and 256 share bucket 255) and one launch
-// sorts every bucket in one workgroup: the bits that vary inside a bucket are few (a tile >= 128's
-// keys 16, [1, 2) 23), so 2-3 LSD passes of 8 bits in LDS order it, and each value goes straight
-// to its position in the full order (position in the kept subset + PrefixDev::delta of its key's
-// class, as kPlace).
-#ifndef GS_CS_WAVES
-#define GS_CS_WAVES 16
-#endif
-constexpr int kCsWaves = GS_CS_WAVES;               // 1024 threads
-constexpr int kCsCap = kCsWaves * 64 * kItems;      // 16384 keys in LDS (128 KB of pairs)
-
-// Stable ranks of one tile of up to W * 64 * IT keys (wave w, item k, lane l = position
-// w*64*IT + k*64 + l; valid below tn) by digit (key >> shift) & 0xff, as rank_tile for W waves:
-// ps[k] = the item's place in the tile's order, s_tdig[d] the tile's count of digit d, s_start[d]
-// its first place.  Waves whose whole range lies past tn rank nothing.  Starts and ends with a
-// barrier.
-template <int W, int IT>
-__device__ __forceinline__ void rank_tile_w(const uint32_t (&kk)[IT], uint32_t tn, int shift, uint32_t (&ps)[IT],
-                                            uint32_t (*s_cnt)[kRadix], uint32_t *s_start, uint32_t *s_wave,
-                                            uint32_t *s_tdig) {
-    static_assert(W * 64 >= kRadix, "one thread per digit");
-    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
-    __syncthreads();  // the previous use of the scratch is done
-    for (int i = threadIdx.x; i < W * kRadix; i += W * 64) (&s_cnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t wbase = wid * (uint32_t)(64 * IT);
-    const uint32_t base = wbase + lane;
-    if (wbase < tn) {  // uniform per wave
-        // items in chunks of CH (the match masks of a chunk, its leaders' returning LDS atomics
-        // back to back, the broadcasts): rank / lead / old for CH items at a time, not all IT
-        constexpr int CH = IT < 4 ? IT : 4;
-#pragma unroll
-        for (int c0 = 0; c0 < IT; c0 += CH) {
-            uint32_t rank[CH], lead[CH], old[CH];
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int k = c0 + j;
-                const bool valid = base + k * 64 < tn;
-                const uint64_t m = match_digit((kk[k] >> shift) & 0xffu, __ballot(valid));
-                rank[j] = count_below(m);
-                lead[j] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
-                old[j] = valid ? (uint32_t)__popcll(m) : 0u;
-            }
-#pragma unroll
-            for (int j = 0; j < CH; ++j) {
-                const int k = c0 + j;
-                const bool valid = base + k * 64 < tn;
-                if (valid && lead[j] == (uint32_t)lane) old[j] = atomicAdd(&s_cnt[wid][(kk[k] >> shift) & 0xffu], old[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < CH; ++j)
-                ps[c0 + j] = rank[j] + (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[j] << 2), (int)old[j]);
-        }
-    }
-    __syncthreads();
-    uint32_t tot = 0;
-    if (d < kRadix) {
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            const uint32_t c = s_cnt[w][d];
-            s_cnt[w][d] = tot;
-            tot += c;
-        }
-        s_tdig[d] = tot;
-    }
-    const uint32_t st = block_excl_scan<W>(d < kRadix ? tot : 0u, s_wave);
-    if (d < kRadix) s_start[d] = st;
-    __syncthreads();
-    if (wbase < tn) {
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const uint32_t dg = (kk[k] >> shift) & 0xffu;
-            ps[k] += s_start[dg] + s_cnt[wid][dg];  // (ps held the rank within the wave's digit)
-        }
-    }
-    __syncthreads();
-}
-
-// the 8-bit LSD passes that order a bucket: the bits below the highest one where its smallest and
-// largest key differ (mn, mx: this thread's extremes; W waves)
-template <int W>
-__device__ __forceinline__ int bucket_passes_w(uint32_t mn, uint32_t mx, uint32_t (*s_mm)[W]) {
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
-    }
-    if (lane == 0) {
-        s_mm[0][wid] = mn;
-        s_mm[1][wid] = mx;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-        mn = min(mn, s_mm[0][w]);
-        mx = max(mx, s_mm[1][w]);
-    }
-    const uint32_t diff = mn ^ mx;
-    return diff ? (32 - __builtin_clz(diff) + 7) / 8 : 0;
-}
-
-// One workgroup per bucket b: its kept keys are (kin, vin)[base, base + m) in input order (the
-// first pass's scatter; base = the kept keys of the buckets before it, m = row_total[b]); sorted
-// stably, each value goes to vout[subset position + pre.delta[class of its key]].  Buckets of at
-// most kCsCap keys sort in registers and LDS; longer ones take the same passes through global
-// memory in kCsCap-key tiles, ping-ponging between (kin, vin) and the scratch (ks, vs) over the
-// bucket's range.
-__global__ __launch_bounds__(kCsWaves * 64) void k_class_sort(uint32_t *__restrict__ kin, uint32_t *__restrict__ vin,
-                                                               uint32_t *__restrict__ ks, uint32_t *__restrict__ vs,
-                                                               uint32_t *__restrict__ vout,
-                                                               const uint32_t *__restrict__ row_total, PrefixDev pre) {
-    constexpr int W = kCsWaves, kThreads = W * 64;
-    __shared__ uint32_t s_k[kCsCap], s_v[kCsCap];
-    __shared__ uint32_t s_cnt[W][kRadix];
-    __shared__ uint32_t s_start[kRadix], s_tdig[kRadix], s_run[kRadix];
-    __shared__ uint32_t s_wave[W];
-    __shared__ uint32_t s_mm[2][W];
-    __shared__ int32_t s_delta[kClasses];
-    __shared__ uint32_t s_bm[2];
-    const int lane = lane_id(), wid = threadIdx.x >> 6, d = threadIdx.x;
-    const uint32_t b = blockIdx.x;
-    {  // the bucket's base in the kept subset and its size
-        const uint32_t r = d < kRadix ? row_total[d] : 0u;
-        const uint32_t ex = block_excl_scan<W>(r, s_wave);
-        if (d == (int)b) {
-            s_bm[0] = ex;
-            s_bm[1] = r;
-        }
-        for (int i = threadIdx.x; i < kClasses; i += kThreads) s_delta[i] = pre.delta[i];
-        __syncthreads();
-    }
-    const uint32_t b0 = s_bm[0], m = s_bm[1];
-    if (m == 0) return;  // uniform
-    const uint32_t base = wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems], vv[kItems], ps[kItems];
-    auto place = [&](uint32_t pos, uint32_t key, uint32_t val) {
-        vout[(uint32_t)((int32_t)(b0 + pos) + s_delta[key_class(key)])] = val;
-    };
-    if (m <= (uint32_t)kCsCap) {  // uniform: registers and LDS
-        uint32_t mn = 0xffffffffu, mx = 0u;
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const uint32_t pos = base + k * 64;
-            kk[k] = pos < m ? kin[b0 + pos] : 0u;
-            vv[k] = pos < m ? vin[b0 + pos] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if (base + k * 64 < m) {
-                mn = min(mn, kk[k]);
-                mx = max(mx, kk[k]);
-            }
-        const int passes = bucket_passes_w<W>(mn, mx, s_mm);
-        for (int p = 0; p < passes; ++p) {
-            rank_tile_w<W, kItems>(kk, m, 8 * p, ps, s_cnt, s_start, s_wave, s_tdig);
-#pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if (base + k * 64 < m) {
-                    s_k[ps[k]] = kk[k];
-                    s_v[ps[k]] = vv[k];
-                }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < kItems; ++k) {
-                const uint32_t pos = base + k * 64;
-                kk[k] = pos < m ? s_k[pos] : 0u;
-                vv[k] = pos < m ? s_v[pos] : 0u;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if (base + k * 64 < m) place(base + k * 64, kk[k], vv[k]);
-        return;
-    }
-    // long bucket: LSD passes through global memory, kCsCap-key tiles in order
-    int passes;
-    {
-        uint32_t mn = 0xffffffffu, mx = 0u;
-        for (uint32_t i = threadIdx.x; i < m; i += kThreads) {
-            const uint32_t k = kin[b0 + i];
-            mn = min(mn, k);
-            mx = max(mx, k);
-        }
-        passes = bucket_passes_w<W>(mn, mx, s_mm);
-    }
-    uint32_t *sk = kin, *sv = vin, *dk = ks, *dv = vs;
-    for (int p = 0; p < passes; ++p) {
-        const int shift = 8 * p;
-        if (d < kRadix) s_run[d] = 0;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += kThreads) atomicAdd(&s_run[(sk[b0 + i] >> shift) & 0xffu], 1u);
-        __syncthreads();
-        {
-            const uint32_t c = d < kRadix ? s_run[d] : 0u;
-            const uint32_t ex = block_excl_scan<W>(c, s_wave);
-            if (d < kRadix) s_run[d] = ex;  // (each thread its own digit)
-        }
-        for (uint32_t t0 = 0; t0 < m; t0 += kCsCap) {
-            const uint32_t tn = min((uint32_t)kCsCap, m - t0);
-#pragma unroll
-            for (int k = 0; k < kItems; ++k) {
-                const uint32_t pos = base + k * 64;
-                kk[k] = pos < tn ? sk[b0 + t0 + pos] : 0u;
-                vv[k] = pos < tn ? sv[b0 + t0 + pos] : 0u;
-            }
-            rank_tile_w<W, kItems>(kk, tn, shift, ps, s_cnt, s_start, s_wave, s_tdig);
-#pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if (base + k * 64 < tn) {
-                    const uint32_t dg = (kk[k] >> shift) & 0xffu;
-                    const uint32_t o = b0 + s_run[dg] + (ps[k] - s_start[dg]);
-                    dk[o] = kk[k];
-                    dv[o] = vv[k];
-                }
-            __syncthreads();
-            if (d < kRadix) s_run[d] += s_tdig[d];
-        }
-        // the pass's stores before the next pass's loads by the other waves (agent-scope release /
-        // acquire: the acquire invalidates this CU's vector L1, which may hold the range's old lines)
-        __threadfence();
-        __syncthreads();
-        __threadfence();
-        uint32_t *t = sk;
-        sk = dk;
-        dk = t;
-        t = sv;
-        sv = dv;
-        dv = t;
-    }
-    for (uint32_t i = threadIdx.x; i < m; i += kThreads) place(i, sk[b0 + i], sv[b0 + i]);
-}
-
 // The prefix sort's class bounds (one workgroup of 256 per tile class; thread j owns buckets
 // [8j, 8j + 8) of every copy): walking the sampled histogram from the largest distance (the
 // front of the list) down, the bucket where the count reaches target / kPrefixSample sets
@@ -1446,261 +1204,6 @@ __global__ __launch_bounds__(256) void k_gather_keys(const float *__restrict__ k
 
 }  // namespace
 
-// ---------------------------------------------------------------- GS_SORT11 (opt-in)
-// Standalone sorts of >= 16M pairs in three LSD passes of 11, 11 and 10 bits (VERDICT r4 item 5:
-// 4 + 3 x 16 bytes of pairs per key against 4 x 16 + 4), reduce-then-scan:
-//   k_upsweep11    a 2048-bin LDS histogram per 8192-key tile, stored tile-major (8 KB per tile,
-//                  one coalesced store);
-//   k_colscan11    per digit, the exclusive prefix over the tiles (in place) and the digit's total:
-//                  a workgroup per 8 digits, its 32 tile groups scanned then offset;
-//   k_downsweep11  sixteen waves of 8 keys per lane: stable ranking by an 11-bit ballot match,
-//                  per-wave 16-bit counters packed two to a word (64 KB, shared with the tile's
-//                  reorder buffer: positions stay in registers across the barrier), the tile's
-//                  2048 prefixes read contiguously, coalesced scatter.
-#ifndef GS_SORT11
-#define GS_SORT11 0
-#endif
-constexpr int kR11 = 2048;
-constexpr int kW11 = 16, kI11 = 8;                 // downsweep: waves, keys per lane
-constexpr int kT11 = kWaveBig * kWaveTile;         // 8192 keys per tile (= kW11 * 64 * kI11)
-static_assert(kW11 * 64 * kI11 == kT11, "one tile size for the three kernels");
-template <int BITS>
-__device__ __forceinline__ uint64_t match_digit_n(uint32_t d, uint64_t active) {
-    uint32_t xlo = 0, xhi = 0;
-#pragma unroll
-    for (int b = 0; b < BITS; ++b) {
-        uint32_t sb = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
-        asm volatile("" : "+v"(sb));
-        const uint64_t bb = __ballot(sb != 0u);
-        xlo = or_xor(xlo, sb, (uint32_t)bb);
-        xhi = or_xor(xhi, sb, (uint32_t)(bb >> 32));
-    }
-    return (((uint64_t)~xhi << 32) | ~xlo) & active;
-}
-
-template <int BITS>
-__global__ __launch_bounds__(kWaveBig * 64) void k_upsweep11(const uint32_t *__restrict__ keys, uint32_t n, int shift,
-                                                             uint32_t *__restrict__ hist) {
-    constexpr int kThreads = kWaveBig * 64, R = 1 << BITS;
-    const uint32_t live = (n + kT11 - 1) / kT11;
-    const uint32_t tile = xcd_tile_rev(live);
-    if (tile >= live) return;  // uniform
-    __shared__ uint32_t s_cnt[R];
-    for (int i = threadIdx.x; i < R; i += kThreads) s_cnt[i] = 0;
-    __syncthreads();
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t base = tile * (uint32_t)kT11 + wid * (uint32_t)kWaveTile + lane;
-    uint32_t kk[kItems];
-#pragma unroll
-    for (int k = 0; k < kItems; ++k) {
-        const uint32_t idx = base + k * 64;
-        kk[k] = idx < n ? keys[idx] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if (base + k * 64 < n) atomicAdd(&s_cnt[(kk[k] >> shift) & (R - 1)], 1u);
-    __syncthreads();
-    for (int d = threadIdx.x; d < R; d += kThreads) hist[(size_t)tile * R + d] = s_cnt[d];
-}
-
-// workgroup g: digits [8 g, 8 g + 8); thread (c = t / 8, d = t % 8) scans tiles [c * per, ...)
-template <int BITS>
-__global__ __launch_bounds__(256) void k_colscan11(uint32_t *__restrict__ hist, uint32_t nb, uint32_t *__restrict__ total) {
-    constexpr int R = 1 << BITS;
-    __shared__ uint32_t s_c[32][8];
-    const int t = threadIdx.x, c = t >> 3, dl = t & 7;
-    const uint32_t d = blockIdx.x * 8u + (uint32_t)dl;
-    const uint32_t per = (nb + 31) / 32, t0 = (uint32_t)c * per, t1 = min(nb, t0 + per);
-    uint32_t sum = 0;
-    for (uint32_t j = t0; j < t1; ++j) sum += hist[(size_t)j * R + d];
-    s_c[c][dl] = sum;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-        const uint32_t v = s_c[q][dl];
-        off += q < c ? v : 0u;
-        tot += v;
-    }
-    for (uint32_t j = t0; j < t1; ++j) {
-        const uint32_t v = hist[(size_t)j * R + d];
-        hist[(size_t)j * R + d] = off;
-        off += v;
-    }
-    if (c == 0) total[d] = tot;
-}
-
-template <int BITS>
-__global__ __launch_bounds__(kW11 * 64) void k_downsweep11(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
-                                                            uint32_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                            uint32_t n, int shift, const uint32_t *__restrict__ hist,
-                                                            const uint32_t *__restrict__ total) {
-    constexpr int W = kW11, kThreads = W * 64, R = 1 << BITS;
-    static_assert(W * (kR11 / 2) * 4 >= kT11 * 8, "the reorder buffer fits in the counters' LDS");
-    const uint32_t live = (n + kT11 - 1) / kT11;
-    const uint32_t tile = xcd_tile(live);
-    if (tile >= live) return;  // uniform
-    __shared__ uint32_t s_cnt[W][kR11 / 2];  // per-wave 16-bit counters, then the tile's keys and values
-    __shared__ uint32_t s_start[R];
-    __shared__ int32_t s_gbase[R];
-    __shared__ uint32_t s_w[W];
-    uint32_t *s_keys = &s_cnt[0][0], *s_vals = &s_cnt[0][0] + kT11;
-    for (int i = threadIdx.x; i < W * (kR11 / 2); i += kThreads) (&s_cnt[0][0])[i] = 0;
-    __syncthreads();
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint32_t tile0 = tile * (uint32_t)kT11;
-    const uint32_t base = tile0 + wid * (uint32_t)(64 * kI11) + lane;
-    uint32_t kk[kI11], vv[kI11];
-#pragma unroll
-    for (int k = 0; k < kI11; ++k) {
-        const uint32_t idx = base + k * 64;
-        kk[k] = idx < n ? kin[idx] : 0u;
-        vv[k] = idx < n ? vin[idx] : 0u;
-    }
-    uint32_t rank[kI11], lead[kI11], old[kI11];
-#pragma unroll
-    for (int k = 0; k < kI11; ++k) {
-        const bool valid = base + k * 64 < n;
-        const uint32_t d = (kk[k] >> shift) & (R - 1);
-        const uint64_t m = match_digit_n<BITS>(d, __ballot(valid));
-        rank[k] = count_below(m);
-        lead[k] = valid ? (uint32_t)__builtin_ctzll(m) : (uint32_t)lane;
-        old[k] = valid ? (uint32_t)__popcll(m) : 0u;
-    }
-    // (a wave holds at most 512 keys of a digit: 16-bit halves never carry)
-#pragma unroll
-    for (int k = 0; k < kI11; ++k)
-        if (base + k * 64 < n && lead[k] == (uint32_t)lane) {
-            const uint32_t d = (kk[k] >> shift) & (R - 1), sh = 16u * (d & 1u);
-            old[k] = (atomicAdd(&s_cnt[wid][d >> 1], old[k] << sh) >> sh) & 0xffffu;
-        }
-#pragma unroll
-    for (int k = 0; k < kI11; ++k) rank[k] += (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lead[k] << 2), (int)old[k]);
-    __syncthreads();
-    // per digit: the waves' exclusive offsets, the tile's digit starts, the global bases
-    constexpr int DPT = (R + kThreads - 1) / kThreads;  // digits per thread (2 or 1)
-    uint32_t tot[DPT], a = 0, g = 0;
-#pragma unroll
-    for (int j = 0; j < DPT; ++j) {
-        const int d = threadIdx.x * DPT + j;
-        uint32_t t = 0;
-        if (d < R) {
-            const uint32_t sh = 16u * ((uint32_t)d & 1u);
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t word = s_cnt[w][d >> 1];
-                const uint32_t c = (word >> sh) & 0xffffu;
-                // (the exclusive offset replaces the count in place; the other half is another
-                // thread's digit -- the pair belongs to one thread when DPT == 2)
-                s_cnt[w][d >> 1] = DPT == 2 ? (sh ? (word & 0xffffu) | (t << 16) : (word & 0xffff0000u) | t) : word;
-                t += c;
-            }
-            g += total[d];
-        }
-        tot[j] = t;
-        a += t;
-    }
-    if (DPT == 1) __syncthreads();  // (one digit per thread: the pair's halves are two threads')
-    if (DPT == 1) {
-        const int d = threadIdx.x;
-        // rewrite both halves of the pair from its even thread, the counts recomputed
-        if ((d & 1) == 0 && d + 1 < R) {
-            uint32_t t0 = 0, t1 = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t word = s_cnt[w][d >> 1];
-                s_cnt[w][d >> 1] = (t0 & 0xffffu) | (t1 << 16);
-                t0 += word & 0xffffu;
-                t1 += word >> 16;
-            }
-        }
-    }
-    const uint32_t ex = block_excl_scan<W>(a, s_w);
-    const uint32_t gex = block_excl_scan<W>(g, s_w);
-    {
-        uint32_t st = ex, gb = gex;
-#pragma unroll
-        for (int j = 0; j < DPT; ++j) {
-            const int d = threadIdx.x * DPT + j;
-            if (d < R) {
-                s_start[d] = st;
-                s_gbase[d] = (int32_t)(gb + hist[(size_t)tile * R + d]) - (int32_t)st;
-                st += tot[j];
-                gb += total[d];
-            }
-        }
-    }
-    __syncthreads();
-    uint32_t pos[kI11];
-#pragma unroll
-    for (int k = 0; k < kI11; ++k) {
-        const uint32_t d = (kk[k] >> shift) & (R - 1), sh = 16u * (d & 1u);
-        pos[k] = s_start[d] + ((s_cnt[wid][d >> 1] >> sh) & 0xffffu) + rank[k];
-    }
-    __syncthreads();  // (the counters' LDS becomes the reorder buffer)
-#pragma unroll
-    for (int k = 0; k < kI11; ++k)
-        if (base + k * 64 < n) {
-            s_keys[pos[k]] = kk[k];
-            s_vals[pos[k]] = vv[k];
-        }
-    __syncthreads();
-    const uint32_t tile_n = min((uint32_t)kT11, n - tile0);
-    for (uint32_t i = threadIdx.x; i < tile_n; i += kThreads) {
-        const uint32_t key = s_keys[i];
-        const uint32_t o = (uint32_t)(s_gbase[(key >> shift) & (R - 1)] + (int32_t)i);
-        kout[o] = key;
-        vout[o] = s_vals[i];
-    }
-}
-
-int sort_pairs11(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, int64_t n, std::string &err,
-                 hipEvent_t start, hipEvent_t stop) {
-    const uint32_t nb = (uint32_t)((n + kT11 - 1) / kT11);
-    if ((size_t)n > sc.alt2_cap || (size_t)nb * kR11 > sc.hist11_cap) {
-        (void)hipStreamSynchronize(s);
-        for (uint32_t **p : {&sc.keys_alt2, &sc.vals_alt2, &sc.hist11})
-            if (*p) (void)hipFree(*p), *p = nullptr;
-        sc.alt2_cap = sc.hist11_cap = 0;
-        if (hipMalloc(&sc.keys_alt2, (size_t)n * 4) != hipSuccess || hipMalloc(&sc.vals_alt2, (size_t)n * 4) != hipSuccess ||
-            hipMalloc(&sc.hist11, (size_t)nb * kR11 * 4) != hipSuccess) {
-            err = "radix sort: out of device memory";
-            return GS_ERR_NOMEM;
-        }
-        sc.alt2_cap = (size_t)n;
-        sc.hist11_cap = (size_t)nb * kR11;
-    }
-    if (!sc.row11 && hipMalloc(&sc.row11, kR11 * 4) != hipSuccess) {
-        err = "radix sort: out of device memory";
-        return GS_ERR_NOMEM;
-    }
-    // keys -> alt -> alt2 -> keys
-    uint32_t *kin[3] = {keys, sc.keys_alt, sc.keys_alt2}, *vin[3] = {vals, sc.vals_alt, sc.vals_alt2};
-    uint32_t *kou[3] = {sc.keys_alt, sc.keys_alt2, keys}, *vou[3] = {sc.vals_alt, sc.vals_alt2, vals};
-    const int shifts[3] = {0, 11, 22};
-    for (int pass = 0; pass < 3; ++pass) {
-        hipEvent_t e0 = pass == 0 ? start : nullptr, e1 = pass == 2 ? stop : nullptr;
-        if (pass == 2) {
-            hipExtLaunchKernelGGL(k_upsweep11<10>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
-                                  (uint32_t)n, shifts[pass], sc.hist11);
-            hipLaunchKernelGGL(k_colscan11<10>, dim3(1024 / 8), dim3(256), 0, s, sc.hist11, nb, sc.row11);
-            hipExtLaunchKernelGGL(k_downsweep11<10>, dim3(xcd_grid(nb)), dim3(kW11 * 64), 0, s, nullptr, e1, 0, kin[pass],
-                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, sc.row11);
-        } else {
-            hipExtLaunchKernelGGL(k_upsweep11<11>, dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, e0, nullptr, 0, kin[pass],
-                                  (uint32_t)n, shifts[pass], sc.hist11);
-            hipLaunchKernelGGL(k_colscan11<11>, dim3(2048 / 8), dim3(256), 0, s, sc.hist11, nb, sc.row11);
-            hipExtLaunchKernelGGL(k_downsweep11<11>, dim3(xcd_grid(nb)), dim3(kW11 * 64), 0, s, nullptr, e1, 0, kin[pass],
-                                  vin[pass], kou[pass], vou[pass], (uint32_t)n, shifts[pass], sc.hist11, sc.row11);
-        }
-    }
-    if (hipGetLastError() != hipSuccess) {
-        err = "radix sort: kernel launch failed";
-        return GS_ERR_HIP;
-    }
-    return GS_OK;
-}
-
 int sort_ensure(SortScratch &sc, int64_t n, std::string &err, hipStream_t s, bool small) {
     // the most tiles of any pass (the small form keeps all four passes' histograms)
     // (small: the bucket pass's 1024-key tiles)
@@ -1753,7 +1256,6 @@ void sort_free(SortScratch &sc) {
     if (sc.hist) (void)hipFree(sc.hist);
     if (sc.row_total) (void)hipFree(sc.row_total);
     if (sc.bkt) (void)hipFree(sc.bkt);
-    if (sc.vals_scr) (void)hipFree(sc.vals_scr);
     sc = SortScratch{};
 }
 
@@ -1785,8 +1287,6 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     }
     int rc = sort_ensure(sc, std::max<int64_t>(n, 1), err, s, small);
     if (rc) return rc;
-    if (GS_SORT11 && !pre && !bins && keys_out && !dev_count && dup_base < 0 && n >= (int64_t)1 << 24)
-        return sort_pairs11(s, sc, keys, vals, n, err, start, stop);
     uint32_t *tile_counts = sc.row_total + kRadix;
     if (n < 1 && !dev_count) {  // no keys: the (zero) bins only
         if (start) (void)hipEventRecord(start, s);
@@ -1841,43 +1341,6 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     PrefixDev pd = pre ? *pre : PrefixDev{};
     pd.frame_count = dev_count;
     pd.cap_all = (uint32_t)n;
-    if (pre && kPrefixClassSort) {
-        // the prefix sort in one scatter pass and one class sort (k_class_sort): 5 launches
-        if (sc.scr_cap < (size_t)n) {
-            if (sc.vals_scr) {
-                (void)hipStreamSynchronize(s);  // in-flight users
-                (void)hipFree(sc.vals_scr);
-            }
-            sc.vals_scr = nullptr;
-            sc.scr_cap = 0;
-            const size_t cap = (size_t)n + (size_t)n / 4 + 4096;
-            if (hipMalloc(&sc.vals_scr, cap * 4) != hipSuccess) {
-                err = "radix sort: out of device memory";
-                return GS_ERR_NOMEM;
-            }
-            sc.scr_cap = cap;
-        }
-        const uint32_t tile = kWaveBig * kWaveTile;
-        const uint32_t nb = (uint32_t)((n + tile - 1) / tile);
-        const uint32_t split = dup_base >= 0 ? (uint32_t)dup_base : kNoSplit;
-        hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
-        hipLaunchKernelGGL((k_upsweep<kWaveBig, true, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, kin,
-                           (uint32_t)n, dev_count, 0, sc.hist, nb, tile_counts, pd, split);
-        auto scan = nb > 4096 ? k_scan_rows<64> : k_scan_rows<4>;
-        hipLaunchKernelGGL(scan, dim3(kRadix + 1), dim3(256), 0, s, sc.hist, nb, (uint32_t)n, dev_count, tile,
-                           sc.row_total, tile_counts, bins, pd, 3);
-        hipLaunchKernelGGL((k_downsweep<kWaveBig, kPairs, true, true>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, kin, vin,
-                           kout, vout, (uint32_t)n, dev_count, 0, sc.hist, nb, sc.row_total, pd, split);
-        // (the kept pairs, by bucket, in the alternate buffers; keys and vals_scr are scratch of long
-        // buckets; the values land in vals)
-        hipExtLaunchKernelGGL(k_class_sort, dim3(kRadix), dim3(kCsWaves * 64), 0, s, nullptr, stop, 0, kout, vout, keys,
-                              sc.vals_scr, vals, sc.row_total, pd);
-        if (hipGetLastError() != hipSuccess) {
-            err = "radix sort: kernel launch failed";
-            return GS_ERR_HIP;
-        }
-        return GS_OK;
-    }
     const int64_t n_sub = pre ? std::min<int64_t>(n, pre->cap_sel) : n;  // passes 1-3 of a prefix sort
     // a kept emission's input (kept->count set); else kept->after_select alone (see KeptSort)
     const bool kept_in = kept && kept->count;
@@ -1958,10 +1421,10 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
             hipExtLaunchKernelGGL((k_downsweep<kWaveBig, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveBig * 64), 0, s, nullptr, e1, 0,
                                   kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (sub && fmt == kPairs)
-            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs, false, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
                                   s, nullptr, e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (sub && fmt == kPlace)
-            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace, false, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
+            hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPlace, false, kSubItems>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0,
                                   s, nullptr, e1, 0, kin, vin, kout, vout, (uint32_t)np, cnt, shift, sc.hist, nb, sc.row_total, pd, split);
         else if (fmt == kPairs)
             hipExtLaunchKernelGGL((k_downsweep<kWaveSmall, kPairs>), dim3(xcd_grid(nb)), dim3(kWaveSmall * 64), 0, s, nullptr, e1,
