@@ -61,6 +61,18 @@ const float kPrefixTurnCos = (float)std::cos(GS_PREFIX_TURN_MDEG * 1e-3 * 3.1415
 // gs::KeptDev) -- bit-exact, but the work it moves into the preprocess and the emission (+21 and
 // +16 us) costs what the sort saves (-36 us) one frame at a time, and more beside another lane's
 // blend (2175-2196 vs 2344-2355 frames/s, profiles/r05/kept_emission_ab.txt)
+// a turned frame selects each tile class by the depths of the tiles its content came from (the
+// camera's rotation since the frames whose blends recorded them: turned_rects), not by its 3 x 3
+// neighbourhood's
+#ifndef GS_PREFIX_TURN_RECTS
+#define GS_PREFIX_TURN_RECTS 1
+#endif
+#ifndef GS_PREFIX_TURN_VIEWS  // the views a turned frame maps its tiles into (0: one per lane)
+#define GS_PREFIX_TURN_VIEWS 0
+#endif
+#ifndef GS_PREFIX_TURN_EDGE
+#define GS_PREFIX_TURN_EDGE 1
+#endif
 #ifndef GS_KEPT_EMIT
 #define GS_KEPT_EMIT 0
 #endif
@@ -71,6 +83,72 @@ static float turn_cos(const float *a, const float *b) {
     for (int c = 0; c < 3; ++c)
         for (int r = 0; r < 3; ++r) tr += a[4 * c + r] * b[4 * c + r];
     return 0.5f * (tr - 1.0f);
+}
+
+// A turned frame's source tiles (gs::TileRects).  The draw's coarse tile t of the view u (float
+// tile dims W/16, H/16, src/Splats.cpp:596) is mapped by the camera's rotation into each of the
+// views[0, m) -- a pixel's ray in u's camera, the world direction, that view's camera, its pixel --
+// and covers the union of the tile rectangles its corners land in there (the translation between
+// the poses is left out: it moves content by a parallax, which the selection's slack absorbs).
+// Content that lay outside a view entirely, or behind it, is unknown (kRectUnknown: the
+// configured target); a footprint partly outside is clamped to the image and widened by a tile.
+// P00, P11 of the projection from vp * view^-1 (glm::perspective: P02 = P12 = 0).
+static void turned_rects(const gs_uniforms *u, const float (*views)[16], int m, gs::TileRects &tr) {
+    auto at = [](const float *a, int r, int c) { return (double)a[4 * c + r]; };
+    // view^-1 = [R^T | -R^T t] (a rigid view matrix); P = vp * view^-1: only P00 and P11 are needed
+    double Rn[3][3], tn[3], inv[4][4] = {};
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) Rn[r][c] = at(u->view, r, c);
+        tn[r] = at(u->view, r, 3);
+    }
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) inv[r][c] = Rn[c][r];
+        inv[r][3] = -(Rn[0][r] * tn[0] + Rn[1][r] * tn[1] + Rn[2][r] * tn[2]);
+    }
+    inv[3][3] = 1.0;
+    double P00 = 0.0, P11 = 0.0;
+    for (int k = 0; k < 4; ++k) {
+        P00 += at(u->vp, 0, k) * inv[k][0];
+        P11 += at(u->vp, 1, k) * inv[k][1];
+    }
+    const double W = u->width, H = u->height, tw = W / 16.0, th = H / 16.0;
+    for (int t = 0; t < 256; ++t) {
+        const int tx = t & 15, ty = t >> 4;
+        double x0 = 1e30, x1 = -1e30, y0 = 1e30, y1 = -1e30;
+        bool unknown = !(P00 != 0.0 && P11 != 0.0);
+        for (int k = 0; k < m && !unknown; ++k) {
+            for (int cn = 0; cn < 4; ++cn) {
+                const double px = (tx + (cn & 1)) * tw, py = (ty + (cn >> 1)) * th;
+                const double v[3] = {(2.0 * px / W - 1.0) / P00, (2.0 * py / H - 1.0) / P11, -1.0};
+                double d[3], w[3];
+                for (int r = 0; r < 3; ++r) d[r] = Rn[0][r] * v[0] + Rn[1][r] * v[1] + Rn[2][r] * v[2];  // R^T v
+                for (int r = 0; r < 3; ++r) w[r] = at(views[k], r, 0) * d[0] + at(views[k], r, 1) * d[1] + at(views[k], r, 2) * d[2];
+                if (!(w[2] < -1e-6)) {  // behind that camera
+                    unknown = true;
+                    break;
+                }
+                const double qx = (P00 * w[0] / -w[2] + 1.0) * 0.5 * W, qy = (P11 * w[1] / -w[2] + 1.0) * 0.5 * H;
+                x0 = std::min(x0, qx);
+                x1 = std::max(x1, qx);
+                y0 = std::min(y0, qy);
+                y1 = std::max(y1, qy);
+            }
+        }
+        uint32_t code = gs::kRectUnknown;
+        // (GS_PREFIX_TURN_EDGE: content that lay wholly outside the views takes the nearest edge
+        // tiles', widened by a tile, as content partly outside does)
+        if (!unknown && (GS_PREFIX_TURN_EDGE || (x1 >= 0.0 && x0 <= W && y1 >= 0.0 && y0 <= H))) {
+            const bool part = x0 < 0.0 || x1 > W || y0 < 0.0 || y1 > H;
+            int a0 = (int)std::floor(x0 / tw), a1 = (int)std::floor(x1 / tw);
+            int b0 = (int)std::floor(y0 / th), b1 = (int)std::floor(y1 / th);
+            if (part) a0 -= 1, a1 += 1, b0 -= 1, b1 += 1;
+            a0 = std::clamp(a0, 0, 15), a1 = std::clamp(a1, 0, 15), b0 = std::clamp(b0, 0, 15), b1 = std::clamp(b1, 0, 15);
+            code = (uint32_t)a0 | ((uint32_t)a1 << 4) | ((uint32_t)b0 << 8) | ((uint32_t)b1 << 12);
+        }
+        uint32_t &wd = tr.w[t >> 1];
+        const int sh = 16 * (t & 1);
+        wd = (wd & ~(0xffffu << sh)) | (code << sh);
+    }
 }
 
 // A frame lane: a stream and the per-frame buffers of the frames it runs.  Consecutive frames
@@ -202,6 +280,11 @@ struct gs_ctx {
     uint64_t prefix_miss_at[2] = {~0ull, ~0ull}; // ... counts at the two misses before the newest
     int prefix_cooldown = 0;
     float prev_view[16] = {};  // the newest frame's view matrix (the prefix sort's turn test)
+    // the view matrices of the newest frames, newest first (a turned frame's source tiles: the
+    // depths it selects by were recorded by the blends of up to that many frames before it)
+    float view_hist[kMaxLanes][16] = {};
+    int view_hist_n = 0;
+    gs::TileRects tile_rects{};  // the newest turned frame's (read at its k_prefix_select launch)
     bool prefix_kept_turned = false;  // prefix_kept came from a frame selected without the depths
     bool have_prev_view = false;
     uint64_t prefix_frames = 0, prefix_redo = 0, prefix_kept = 0, prefix_E = 0;
@@ -1327,6 +1410,14 @@ int render_spec(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         // kept to the configured target instead (a fast pan missed on nearly every frame)
         pd.use_depth = ctx->have_prev_view && turn_cos(ctx->prev_view, u->view) < kPrefixTurnCos ? 0 : 1;
         sel_turned = pd.use_depth == 0;
+        if (sel_turned && GS_PREFIX_TURN_RECTS && ctx->view_hist_n > 0) {
+            // the depths come from the blends of up to nlanes frames back: each tile's sources in all
+            // of those views
+            turned_rects(u, ctx->view_hist,
+                         std::min(ctx->view_hist_n, GS_PREFIX_TURN_VIEWS > 0 ? GS_PREFIX_TURN_VIEWS : ctx->nlanes),
+                         ctx->tile_rects);
+            pd.rects = &ctx->tile_rects;
+        }
         pd.cap_sel = cap_for(sel_turned);
         pd.n = scene->n;
         pd.clean = (flags & GS_FLAG_CLEAN) ? 1 : 0;
@@ -1552,6 +1643,9 @@ int render_impl(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32
         if (rc == GS_OK) {
             std::memcpy(ctx->prev_view, u->view, sizeof(ctx->prev_view));
             ctx->have_prev_view = true;
+            for (int i = kMaxLanes - 1; i > 0; --i) std::memcpy(ctx->view_hist[i], ctx->view_hist[i - 1], sizeof(ctx->view_hist[0]));
+            std::memcpy(ctx->view_hist[0], u->view, sizeof(ctx->view_hist[0]));
+            ctx->view_hist_n = std::min(ctx->view_hist_n + 1, kMaxLanes);
         }
         return rc;
     };

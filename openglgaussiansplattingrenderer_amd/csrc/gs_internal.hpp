@@ -75,6 +75,16 @@ constexpr int kPrefixHistCopies = 2;
 // word of bucket b in its class's histogram: consecutive buckets on different cache lines
 __host__ __device__ constexpr uint32_t prefix_slot(uint32_t b) { return (b & 7u) * (kPrefixBuckets / 8) + (b >> 3); }
 constexpr int kPrefixCopies = 16;  // selected-count copies (spread same-address atomics)
+// A turned frame's source tiles (PrefixDev::rects): for each tile t of the new view, the rectangle of
+// tiles of the views the recorded depths came from that its content was in (the camera's rotation
+// maps the tile's corners there; host-computed).  Tile t: 16 bits of word t / 2 (t odd: the high
+// half): x0 | x1 << 4 | y0 << 8 | y1 << 12, or 0xffff -- the content came from outside those views
+// (no depth describes it: the configured target).
+struct TileRects {
+    uint32_t w[128];
+};
+constexpr uint32_t kRectUnknown = 0xffffu;
+
 struct PrefixDev {
     uint32_t *hist;    // [kPrefixHistCopies][256][kPrefixBuckets] sampled counts (zero between frames)
     uint32_t *theta;   // [kClasses] inclusive key bound of the kept keys
@@ -92,8 +102,10 @@ struct PrefixDev {
     // min(target, 2 * depth + kPrefixDepthSlack): lists the blends read shallowly keep less.
     uint32_t *depth;
     int32_t use_depth;  // 0: the camera turned since the frame before (the depths describe another
-                        // view): each class takes its tile neighbourhood's deepest depth
+                        // view): each class takes the deepest depth of the tiles its content came
+                        // from (rects), or without rects of its 3 x 3 neighbourhood
                         // (GS_PREFIX_TURN_NB); its blend still records them
+    const TileRects *rects;  // host memory, read at k_prefix_select's launch (by value), or null
     int32_t n;         // splats of the scene (the reference's culled entries: n - V)
     int32_t clean;     // GS_FLAG_CLEAN (no culled entries)
     // GS_DRAW_SBOX: the last pass also writes each placed value's cull box at its position

@@ -1513,6 +1513,20 @@ __device__ __forceinline__ int slot_y(uint32_t s) {
 #ifndef GS_CULL_SPARSE
 #define GS_CULL_SPARSE 6
 #endif
+// GS_DRAW_PRIO > 0: a sub-block's wave raises its issue priority (s_setprio 1, 2, 3) each time it
+// has batched another GS_DRAW_PRIO box survivors.  The blend's span is set by its heaviest
+// sub-blocks (the most survivors: ~0.7 us each beside six other waves of the SIMD), which start
+// with the first dispatch and finish alone: the light trace of C3 (tools/timeline.py) holds ~6,200
+// blocks resident for half the span and fewer and fewer after; the heavy waves' own pace sets the end.
+#ifndef GS_DRAW_PRIO
+#define GS_DRAW_PRIO 0
+#endif
+#ifndef GS_DRAW_SWALK
+#define GS_DRAW_SWALK 0
+#endif
+#ifndef GS_DRAW_LIGHT_TRACE
+#define GS_DRAW_LIGHT_TRACE 0
+#endif
 #ifndef GS_DRAW_WAVES
 #define GS_DRAW_WAVES 7
 #endif
@@ -1521,7 +1535,7 @@ __device__ __forceinline__ int slot_y(uint32_t s) {
 // 16x16 form on the same image, each walking its tile's list for 64 pixels.  Frames whose blend
 // is latency-bound (a few thousand short-lived sub-blocks, C2 / the small C5 views) take it; a
 // pixel's arithmetic and its survivor order are the same, so the image is the same bit for bit.
-template <bool FAST_EXP, bool STATS, bool SMALL>
+template <bool FAST_EXP, bool STATS, bool SMALL, bool SBOX>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVES))) void k_draw(DrawParams P, const uint32_t *__restrict__ bins,
                                              const uint32_t *__restrict__ vals,
                                              const uint2 *__restrict__ cullbox,
@@ -1531,6 +1545,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // pixel state, pixel id = 16*y + x in the sub-block; a pixel is done (:129-133) iff its
     // w >= 0.99 (pixels outside the image start at w = 1)
     constexpr int SB = SMALL ? 8 : 16;  // sub-block side
+    // GS_DRAW_LIGHT_TRACE (diagnostic builds): the STATS form records only each block's times, list
+    // steps, survivors and batches -- the per-survivor counters roughly doubled the kernel's span
+    constexpr bool STATS_FULL = STATS && !GS_DRAW_LIGHT_TRACE;
     __shared__ float4 s_col[SMALL ? 1 : 256];
     // one survivor's blend events: power and pixel id (split); 5760 B of LDS per wave in all
     // -> 7 waves/SIMD
@@ -1723,6 +1740,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     bool cfin = true;           // every colour of the batch is finite (uniform)
     uint32_t qn = 0;            // survivors queued (uniform)
     bool inflight = false;      // a batch's data gather is in flight (uniform)
+    uint32_t nsurv = 0, prio = 0;  // GS_DRAW_PRIO: box survivors batched so far, the wave's priority
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -1744,7 +1762,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const uint32_t idmax = (uint32_t)max(P.n - 1, 0);
     // (GS_DRAW_SBOX, a prefix-sorted frame: the box at the entry's position, read in list order;
     // one load either way -- the base and offset are selected, not the load)
-    const bool sorted_box = GS_DRAW_SBOX && P.sbox != nullptr;
+    // (SBOX: the launch's P.sbox is set -- a template parameter, so that the positional walk below
+    // can issue a chunk's box load with its index load)
+    constexpr bool sorted_box = SBOX;
     const uint2 *box_base = sorted_box ? P.sbox - 1 : cullbox;
     auto gather_box = [&](uint32_t v, uint32_t off, uint32_t &vb, uint2 &bx) {
         vb = min(v, idmax);
@@ -1771,6 +1791,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         Dd = SurvData{ld.mx, ld.my, ld.a, ld.b, ld.c, ld.o, 0.0f};  // thr: once the data arrived (blend_batch)
         Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
         bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
+        if (GS_DRAW_PRIO) {  // (see GS_DRAW_PRIO) the wave's issue priority by the survivors it took on
+            nsurv += bn;
+            const uint32_t lvl = min(3u, nsurv / (uint32_t)(GS_DRAW_PRIO + 0));
+            if (lvl != prio) {  // uniform, at most three times per block
+                prio = lvl;
+                if (lvl == 1) __builtin_amdgcn_s_setprio(1);
+                else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(3);
+            }
+        }
         if (qn > 64u) {  // uniform, rare
             const uint32_t r = s_q[64 + lane];
             wave_lds_sync();
@@ -1799,7 +1829,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         // a survivor saturated a pixel (rare): the done masks again from the pixel state; a stop
         // hands the survivors left back in keep and ends the loop
         auto refresh = [&]() {
-            if (STATS) ++st_refresh;
+            if (STATS_FULL) ++st_refresh;
             wave_lds_sync();
             D0 = ballot(s_col[qbase + kQuad[0]].w >= 0.99f);
             D1 = ballot(s_col[qbase + kQuad[1]].w >= 0.99f);
@@ -1838,7 +1868,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             const uint32_t e0 = (uint32_t)__popcll(b0), e1 = (uint32_t)__popcll(b1);
             const uint32_t e2 = (uint32_t)__popcll(b2), e3 = (uint32_t)__popcll(b3);
             const uint32_t nev = e0 + e1 + e2 + e3;
-            if (STATS) {
+            if (STATS_FULL) {
                 ++st_kit;
                 const int active = 256 - __popcll(D0) - __popcll(D1) - __popcll(D2) - __popcll(D3);
                 st_kit64 += active <= 64 ? 1 : 0;
@@ -1966,7 +1996,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             const float dx = sfx - mx, dy = sfy - my;
             const float p = -0.5f * ((ca * dx) * dx + (cc * dy) * dy) - (cbv * dx) * dy;
             const uint64_t nb = SA & ballot(needs(p, thr));
-            if (STATS) {
+            if (STATS_FULL) {
                 ++st_kit;
                 ++st_kit64;
                 ++st_kit128;
@@ -2032,7 +2062,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     };
     // prologue: chunk 0 index-loaded and box-gathered, chunk 1 index-loaded
     int base = start;
-    if (base < end && !all_done) {  // uniform
+    if (SBOX && GS_DRAW_SWALK && base < end && !all_done) {  // uniform
+        // the positional walk (sorted boxes): a chunk's index and box loads depend only on its
+        // position, so both issue two steps before its test (the gather form issues the box one
+        // step before: it needs the index)
+        auto load_pos = [&](int b, uint32_t &v, uint2 &bx) {
+            uint32_t off;
+            load_idx(b, v, off);
+            bx = *at(box_base, off << 3);
+        };
+        load_pos(base, Vi[0], Bx[0]);
+        load_pos(base + 64, Vi[1], Bx[1]);
+        auto step = [&](auto U) {
+            constexpr int u = decltype(U)::value;
+            test_and_queue(base, min(Vi[u], idmax), Bx[u]);  // chunk c
+            load_pos(base + 128, Vi[u], Bx[u]);              // chunk c+2
+            if (STATS) ++st_iter;
+            if (inflight) blend_batch();
+            base += 64;
+            if (qn >= kBatch || (base >= end && qn)) issue_batch();  // uniform
+            return (base < end || inflight) && !all_done;
+        };
+        for (;;) {
+            if (!step(std::integral_constant<int, 0>{})) break;
+            if (!step(std::integral_constant<int, 1>{})) break;
+        }
+    } else if (base < end && !all_done) {  // uniform
         uint32_t v0, o0;
         load_idx(base, v0, o0);
         load_idx(base + 64, Vi[1], Oi[1]);
@@ -2230,12 +2285,13 @@ void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, bool small, 
     // margin blocks run
     const int margin = P.W * P.H - P.coverW * P.coverH;
     const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
-#define GS_DRAW(F, S, M)                                                                                         \
-    hipExtLaunchKernelGGL((k_draw<F, S, M>), grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, \
-                          colour, out, stats, fr.h_totals)
-#define GS_DRAW2(F, S) \
-    if (small) GS_DRAW(F, S, true); \
-    else GS_DRAW(F, S, false)
+    // (GS_DRAW_SBOX off: the sorted boxes are never set, see the frame paths)
+    auto go = [&](auto kern) {
+        hipExtLaunchKernelGGL(kern, grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, colour, out,
+                              stats, fr.h_totals);
+    };
+#define GS_DRAW(F, S, M) (P.sbox ? go(k_draw<F, S, M, true>) : go(k_draw<F, S, M, false>))
+#define GS_DRAW2(F, S) (small ? GS_DRAW(F, S, true) : GS_DRAW(F, S, false))
     if (stats) {
         if (fast_exp) GS_DRAW2(true, true);
         else GS_DRAW2(false, true);

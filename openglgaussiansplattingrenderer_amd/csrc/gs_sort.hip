@@ -1116,18 +1116,29 @@ __global__ __launch_bounds__(kWaveSmall * 64) void k_bucket_sort(uint32_t *__res
 // front of the list) down, the bucket where the count reaches target / kPrefixSample sets
 // theta = the class bound - that bucket's smallest distance; a class sampled less keeps every
 // key.  The histogram is cleared for the next frame.
-__global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre) {
+__global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre, TileRects tr, int use_rects) {
     constexpr int kB = kPrefixBuckets / 256;  // buckets per thread (8)
     __shared__ uint32_t s_w[4];
+    __shared__ uint32_t s_dep;
     const uint32_t c = blockIdx.x, j = threadIdx.x;
     static_assert(kB == 8, "prefix_slot puts bucket 8j + k at word k * (kPrefixBuckets / 8) + j");
     uint32_t v[kB] = {};
-    // a frame whose camera turned since the frame before (use_depth 0): the depths recorded at the
-    // other pose describe content that has moved by a fraction of a tile, so class c takes the
-    // deepest of its 3 x 3 tile neighbourhood (with twice the slack) instead of its own
+    // a frame whose camera turned since the frame before (use_depth 0): the depths were recorded at
+    // other poses, where this tile's content sat elsewhere -- class c takes the deepest depth of the
+    // tiles it came from (tr: the camera's rotation maps the tile there, host side; content from
+    // outside those views: the configured target), or without them of its 3 x 3 neighbourhood
     const uint32_t own = pre.depth ? pre.depth[c] : 0u;
     uint32_t dep_nb = 0;
-    if (pre.depth && GS_PREFIX_TURN_NB && !pre.use_depth) {
+    if (pre.depth && !pre.use_depth && use_rects) {  // uniform
+        const uint32_t r = (tr.w[c >> 1] >> (16u * (c & 1u))) & 0xffffu;
+        if (j == 0) s_dep = 0;
+        __syncthreads();
+        const uint32_t x = j & 15u, y = j >> 4;
+        if (r != kRectUnknown && x >= (r & 15u) && x <= ((r >> 4) & 15u) && y >= ((r >> 8) & 15u) && y <= (r >> 12))
+            atomicMax(&s_dep, pre.depth[j]);
+        __syncthreads();
+        dep_nb = r == kRectUnknown ? 0u : s_dep;  // (0: the target)
+    } else if (pre.depth && GS_PREFIX_TURN_NB && !pre.use_depth) {
         const int tx = (int)(c & 15u), ty = (int)(c >> 4);
         constexpr int ry = GS_PREFIX_TURN_NB == 3 ? 0 : 1;  // (3: the row neighbours only)
 #pragma unroll
@@ -1345,7 +1356,8 @@ int sort_pairs(hipStream_t s, SortScratch &sc, uint32_t *keys, uint32_t *vals, i
     // a kept emission's input (kept->count set); else kept->after_select alone (see KeptSort)
     const bool kept_in = kept && kept->count;
     if (pre) {  // the class bounds from the keys the emission sampled (kept: the next frame's)
-        hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd);
+        hipExtLaunchKernelGGL(k_prefix_select, dim3(256), dim3(256), 0, s, start, nullptr, 0, pd,
+                              pd.rects ? *pd.rects : TileRects{}, pd.rects ? 1 : 0);
         start = nullptr;
     }
     // passes 1-3 in the pass-0 form (8 waves, 8192-key tiles) too for sorts of 16M keys or more:

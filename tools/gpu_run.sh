@@ -35,10 +35,16 @@ ab)
   fi
   shift
   one() {
-    timeout -k 10 200 python bench.py --no-cpu-baseline --no-sort-bench --no-sweep "$@" > $O/ab_$v$i.json 2> $O/ab.err || { tail -5 $O/ab.err; return 1; }
+    # (AB_SWEEP=1: with the camera sweeps, their ratios against the same poses static printed too)
+    local sw=--no-sweep; [ -n "$AB_SWEEP" ] && sw=
+    timeout -k 10 300 python bench.py --no-cpu-baseline --no-sort-bench --no-facade $sw "$@" > $O/ab_$v$i.json 2> $O/ab.err || { tail -5 $O/ab.err; return 1; }
     python3 -c "
 import json; d=json.load(open('$O/ab_$v$i.json')); fr=d['frame']
-print('$v', d['value'], 'serial', fr['serial_ms_per_frame'], 'draw', d['roofline']['avg_launch_ms'], {k: round(x, 4) for k, x in fr['stage_ms'].items()})"
+print('$v', d['value'], 'serial', fr['serial_ms_per_frame'], 'draw', d['roofline']['avg_launch_ms'], {k: round(x, 4) for k, x in fr['stage_ms'].items()})
+sw = fr.get('camera_sweep') or {}
+for k, r in sw.items():
+    if isinstance(r, dict) and 'prefix' in r:
+        print('   sweep', k, 'vs_static_same_poses', r['prefix']['vs_static_same_poses'], 'again', r['prefix']['rendered_again'], 'kept', r['prefix']['kept_frac_last'], 'fps', r['prefix']['frames_per_s'])"
   }
   for i in 1 2; do
     v=A; cp $L/libgsplat_hip_old.so $L/libgsplat_hip.so; one "$@" || break
