@@ -1556,7 +1556,53 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
-    const int L = blockIdx.x;
+    int L = blockIdx.x;
+    // GS_DRAW_SPLIT: the sub-blocks the lane's previous frame found heaviest are blended as four 8x8
+    // quadrants (one pixel per lane, the sparse step from the start): quadrant 0 by the sub-block's
+    // own workgroup, 1-3 by helper workgroups at the front of the grid (dispatched first).  Any
+    // split gives the same pixels: each pixel still blends its own tile's list in order.
+    constexpr bool kSplit = !SMALL && GS_DRAW_SPLIT > 0;
+    int quad = -1;          // the quadrant this workgroup blends, -1: the whole sub-block (uniform)
+    int t = 0, sub = 0;
+    bool helper = false;
+    // the helper list belongs to a frame of this size (else no sub-block is split)
+    const bool split_on = kSplit && P.split_in && P.list_in[kSplitMax + 1] == (uint32_t)P.W &&
+                          P.list_in[kSplitMax + 2] == (uint32_t)P.H && P.list_in[kSplitMax + 3] == (uint32_t)P.nbx;
+    if (kSplit && P.split_in) {
+        if (L == 0 && threadIdx.x == 0) {  // this frame's list is empty; the one after next starts empty
+            P.list_reset[kSplitMax] = 0u;
+            P.list_out[kSplitMax + 1] = (uint32_t)P.W;
+            P.list_out[kSplitMax + 2] = (uint32_t)P.H;
+            P.list_out[kSplitMax + 3] = (uint32_t)P.nbx;
+        }
+        if (L < P.nhelp) {  // uniform: a helper
+            const uint32_t e = (uint32_t)L / 3u;
+            if (!split_on || e >= min(P.list_in[kSplitMax], (uint32_t)kSplitMax)) return;
+            const uint32_t ts = P.list_in[e];
+            t = (int)(ts >> 16);
+            sub = (int)(ts & 0xffffu);
+            if (t >= kTiles * kTiles || sub >= nsub) return;
+            quad = L % 3 + 1;
+            helper = true;
+        }
+        L -= P.nhelp;
+    }
+    // a sub-block's workgroup: its split verdict for the lane's next frame -- heavy ones join that
+    // frame's helper list (at most kSplitMax; a sub-block is split iff it is in the list)
+    auto finish_block = [&](bool heavy) __attribute__((always_inline)) {
+        if (!kSplit || !P.split_in || helper) return;
+        if (threadIdx.x == 0) {
+            bool in = false;
+            if (heavy) {
+                const uint32_t i = atomicAdd(&P.list_out[kSplitMax], 1u);
+                if (i < (uint32_t)kSplitMax) {
+                    P.list_out[i] = ((uint32_t)t << 16) | (uint32_t)sub;
+                    in = true;
+                }
+            }
+            P.split_out[t * nsub + sub] = in ? 1 : 0;
+        }
+    };
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
         // drawn coverage (Q9: the reference dispatches (W/32)x(H/32) groups of 32x32); done here
         // instead of a memset launch
@@ -1579,15 +1625,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         }
         return;
     }
-    const int xcd = L & 7, kk = L >> 3;
-    // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
-    const int t = (int)bins[256 + xcd + 8 * (kk / nsub)];
-    const int sub = kk - (kk / nsub) * nsub;
+    if (!helper) {
+        const int xcd = L & 7, kk = L >> 3;
+        // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
+        t = (int)bins[256 + xcd + 8 * (kk / nsub)];
+        sub = kk - (kk / nsub) * nsub;
+        if (split_on && P.split_in[t * nsub + sub]) quad = 0;
+    }
     const int tx = t & 15, ty = t >> 4;
     const int sby = sub / P.nbx, sbx = sub - sby * P.nbx;
     const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
     const int x0 = P.xb[tx] + sbx * SB, y0 = P.yb[ty] + sby * SB;
-    if (x0 >= xe || y0 >= ye) return;  // uniform: sub-block beyond this tile
+    if (x0 >= xe || y0 >= ye) {  // uniform: sub-block beyond this tile
+        finish_block(false);
+        return;
+    }
     const int x1 = min(x0 + SB, xe), y1 = min(y0 + SB, ye);
     const int lane = threadIdx.x;
     const int pxa = x0 + 2 * (lane & 7), pya = y0 + 2 * (lane >> 3);
@@ -1616,8 +1668,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int wend = end;
     if (P.prefix) end = min(end, (int)min(bins[kBinsLimit + t], 0x7fffffffu));
     const int qmax = max(E - 1, 0);
-    // pixels outside the image count as done
-    bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
+    // pixels outside the image count as done (and, split, those of the other quadrants: a lane's
+    // 2x2 quad lies in one quadrant)
+    const int lquad = ((lane & 7) >= 4 ? 1 : 0) + ((lane >> 3) >= 4 ? 2 : 0);
+    const bool mine = !kSplit || quad < 0 || lquad == quad;
+    bool d00 = !in00 || !mine, d10 = !in10 || !mine, d01 = !in01 || !mine, d11 = !in11 || !mine;
 #if GS_DRAW_LANEMAJOR
     // the pixel states are lane-major: the state of the lane's value k (pixel (pxa + k % 2,
     // pya + k / 2)) is slot 64 k + lane -- a value's events, taken in lane order, read and write
@@ -1741,6 +1796,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     uint32_t qn = 0;            // survivors queued (uniform)
     bool inflight = false;      // a batch's data gather is in flight (uniform)
     uint32_t nsurv = 0, prio = 0;  // GS_DRAW_PRIO: box survivors batched so far, the wave's priority
+    uint32_t nsurv_all = 0;        // GS_DRAW_SPLIT: box survivors batched (this frame's verdict)
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -1791,6 +1847,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         Dd = SurvData{ld.mx, ld.my, ld.a, ld.b, ld.c, ld.o, 0.0f};  // thr: once the data arrived (blend_batch)
         Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
         bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
+        if (kSplit) nsurv_all += bn;
         if (GS_DRAW_PRIO) {  // (see GS_DRAW_PRIO) the wave's issue priority by the survivors it took on
             nsurv += bn;
             const uint32_t lvl = min(3u, nsurv / (uint32_t)(GS_DRAW_PRIO + 0));
@@ -2135,22 +2192,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
        // spilled there, a private segment in the dominant kernel)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + 2 * (l2 & 7), qy = y0 + 2 * (l2 >> 3);
+        // (split: only this workgroup's quadrant)
+        const bool wr = !kSplit || quad < 0 || (((l2 & 7) >= 4 ? 1 : 0) + ((l2 >> 3) >= 4 ? 2 : 0)) == quad;
 #if GS_DRAW_LANEMAJOR
         const int qb = l2, q1 = 64, q2 = 128, q3 = 192;
 #else
         const int qb = 32 * (l2 >> 3) + 2 * (l2 & 7), q1 = 1, q2 = 16, q3 = 17;
 #endif
         uint32_t *row0 = out + (size_t)qy * P.W + qx, *row1 = row0 + P.W;
-        if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
-        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + q1]);
-        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + q2]);
-        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
+        if (wr && qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
+        if (wr && qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + q1]);
+        if (wr && qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + q2]);
+        if (wr && qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
     }
     }
+    // the verdict for the lane's next frame: split when this sub-block took on GS_DRAW_SPLIT box
+    // survivors or more (a quadrant of a split one: half that -- a quadrant sees about half)
+    finish_block(quad < 0 ? nsurv_all >= (uint32_t)GS_DRAW_SPLIT : nsurv_all >= (uint32_t)GS_DRAW_SPLIT / 2);
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        if (L < kDrawTraceBlocks) {
-            uint32_t *tr = reinterpret_cast<uint32_t *>(stats) + kDrawTraceWords * L;
+        if (blockIdx.x < (unsigned)kDrawTraceBlocks) {
+            uint32_t *tr = reinterpret_cast<uint32_t *>(stats) + kDrawTraceWords * blockIdx.x;
             tr[0] = (uint32_t)st_t0;
             tr[1] = (uint32_t)t1;
             tr[2] = (uint32_t)st_iter;
@@ -2284,7 +2346,7 @@ void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, bool small, 
     // (see k_draw), then the margin blocks (256 uncovered pixels each); with no coverage only
     // margin blocks run
     const int margin = P.W * P.H - P.coverW * P.coverH;
-    const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
+    const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256 + (P.split_in ? P.nhelp : 0), 1));
     // (GS_DRAW_SBOX off: the sorted boxes are never set, see the frame paths)
     auto go = [&](auto kern) {
         hipExtLaunchKernelGGL(kern, grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, colour, out,
