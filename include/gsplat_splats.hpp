@@ -151,6 +151,38 @@ inline int GPURadixSort(unsigned histogramProgram, unsigned prefixSumProgram, un
                         histogramBuffer, size, workGroupCount, workGroupSize, buffer);
 }
 
+// Splats::numDuplicates (include/Splats.h:56: a public int the reference's gpuRender leaves
+// holding the frame's count, mapped back from its atomic counter every frame,
+// src/Splats.cpp:579-583).  gpuRender here does not wait for its frame, so the count is fetched
+// when it is read: reading it after a gpuRender waits for the frames in flight (gs_sync) and gives
+// the newest frame's duplicates -- as exact as the reference's, stalling only when it is read.
+class DuplicateCount {
+  public:
+    operator int() const {
+        if (pending_) {
+            gs_frame_stats st{};
+            if (gs_sync(ctx_) == GS_OK && gs_seen_stats(ctx_, &st) == GS_OK) value_ = (int)st.duplicates;
+            pending_ = false;
+        }
+        return value_;
+    }
+    DuplicateCount &operator=(int v) {
+        value_ = v;
+        pending_ = false;
+        return *this;
+    }
+
+  private:
+    friend class Splats;
+    void newest_frame_of(gs_ctx *ctx) {  // a frame was enqueued: its count is fetched when read
+        ctx_ = ctx;
+        pending_ = true;
+    }
+    mutable int value_ = 0;
+    mutable bool pending_ = false;
+    gs_ctx *ctx_ = nullptr;
+};
+
 // include/Splats.h:29-124
 class Splats {
   public:
@@ -191,9 +223,9 @@ class Splats {
     // src/Splats.cpp:587-597.  One frame enqueued without a host round trip: gs_render of the
     // uniforms into the back texture of a ring of kTextures (the newest frame's becomes
     // texture()), no stats pointer, no glFinish -- the frame's entry count stays on the device and
-    // frames overlap on the context's lanes (Context::setLanes).  numDuplicates is the count of the
-    // newest frame the host has seen (gs_seen_stats: up to the lanes behind; the reference maps
-    // its atomic counter back every frame, stalling, src/Splats.cpp:579-583).  The stage methods
+    // frames overlap on the context's lanes (Context::setLanes).  numDuplicates is this frame's
+    // count, fetched when it is read (DuplicateCount: the read waits for the frames in flight; the
+    // reference maps its atomic counter back every frame, stalling, src/Splats.cpp:579-583).  The stage methods
     // below keep the reference's staged semantics (one readback per frame) for callers that use
     // them one by one.  The frame is complete after Context::finish() or any readback.
     void gpuRender(const mat4 &viewMatrix, int width, int height, float focal_x, float focal_y, float tan_fov_x,
@@ -205,8 +237,7 @@ class Splats {
         texture_ = back;
         width_ = width;
         height_ = height;
-        gs_frame_stats st{};
-        if (gs_seen_stats(ctx_->get(), &st) == GS_OK) numDuplicates = (int)st.duplicates;
+        numDuplicates.newest_frame_of(ctx_->get());
     }
     // src/Splats.cpp:542-585 (+ emission; the duplicate count is exact, not capped)
     void preprocess(const mat4 &viewMatrix, int width, int height, float focal_x, float focal_y, float tan_fov_x,
@@ -252,7 +283,7 @@ class Splats {
     void setFlags(uint32_t f) { flags_ = f; }
 
     int numSplats{};
-    int numDuplicates{};
+    DuplicateCount numDuplicates;  // reads as an int (see DuplicateCount)
     std::vector<vec4> means3D;
     std::vector<vec4> colours;
     std::vector<float> sphericalHarmonics;  // never filled (include/Splats.h:59)

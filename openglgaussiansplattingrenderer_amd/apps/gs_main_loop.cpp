@@ -85,13 +85,16 @@ int main(int argc, char **argv) {
         if (!f || std::fwrite(img_ahead.data(), 1, img_ahead.size(), f) != img_ahead.size()) return 6;
         std::fclose(f);
     }
+    // numDuplicates read after the loops: the newest frame's (the last pose), as the reference's
+    // gpuRender leaves it (src/Splats.cpp:579-583)
+    const int dups = splats.numDuplicates;
     gs_frame_stats st{};
     gs_last_stats(ctx.get(), &st);
     std::printf("{\"frames\": %d, \"warmup\": %d, \"lanes\": %d, \"turn_deg_per_frame\": %g, \"splats\": %d, "
                 "\"E\": %lld, \"numDuplicates\": %d, \"serial_fps\": %.3f, \"serial_ms_per_frame\": %.4f, "
                 "\"ahead_fps\": %.3f, \"ahead_ms_per_frame\": %.4f, \"last_images_identical\": %s, \"load_s\": %.3f, "
                 "\"presented\": %s}\n",
-                frames, warmup, lanes, turn, splats.numSplats, (long long)st.entries, splats.numDuplicates,
+                frames, warmup, lanes, turn, splats.numSplats, (long long)st.entries, dups,
                 frames / s_serial, s_serial / frames * 1e3, frames / s_ahead, s_ahead / frames * 1e3,
                 same ? "true" : "false", load_s, shown ? "true" : "false");
     return same ? 0 : 1;

@@ -97,6 +97,11 @@ int main(int argc, char **argv) {
         const std::vector<uint8_t> img = splats.display();
         std::ofstream(argv[2], std::ios::binary).write((const char *)img.data(), (std::streamsize)img.size());
         std::cout << "rendered C1: duplicates " << splats.numDuplicates << std::endl;
+        // numDuplicates after gpuRender is that frame's count: the staged preprocess of the same
+        // pose (src/Splats.cpp:542-585's readback) gives the same
+        const int d_frame = splats.numDuplicates;
+        splats.preprocess(view, 256, 256, u.focal_x, u.focal_y, u.tan_fov_x, u.tan_fov_y, vp);
+        EXPECT(d_frame == splats.numDuplicates);
     }
     {  // a Context made current here and destroyed on another thread is no longer current here
         gs::Context *other = new gs::Context(0);

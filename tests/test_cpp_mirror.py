@@ -71,6 +71,9 @@ def test_main_loop_c2_matches_python(tmp_path, turn):
     cam.rotateRight(turn * (frames - 1))
     sp.render_uniforms(cam.uniforms())
     assert d["E"] == sp.stats.entries
+    # Splats::numDuplicates read after the frames is the last frame's count (it lagged by
+    # the frames in flight when taken at gpuRender time; with a turning camera every pose's differs)
+    assert d["numDuplicates"] == sp.stats.duplicates, (d, sp.stats.duplicates)
     img = np.fromfile(img_path, np.uint8).reshape(H, W, 4)
     assert np.array_equal(img, sp.texture())
     ctx.close()
