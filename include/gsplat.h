@@ -228,8 +228,8 @@ int gs_render(gs_ctx *ctx, const gs_scene *scene, const gs_uniforms *u, uint32_t
 int gs_last_stats(gs_ctx *ctx, gs_frame_stats *stats);
 /* the same counts of the newest frame whose counts the host has already seen, without waiting:
  * behind gs_render's frames in flight by up to the number of lanes (the reference reads the count
- * back each frame, src/Splats.cpp:579-583, stalling its pipeline; the C++ facade's gpuRender
- * fills Splats::numDuplicates from this) */
+ * back each frame, src/Splats.cpp:579-583, stalling its pipeline; the C++ facade's
+ * Splats::numDuplicates reads it after a gs_sync, when it is read) */
 int gs_seen_stats(gs_ctx *ctx, gs_frame_stats *stats);
 
 /* stage-level entry points mirroring the reference's Splats methods */
