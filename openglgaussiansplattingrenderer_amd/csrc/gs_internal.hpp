@@ -202,7 +202,8 @@ struct DrawParams {
     const uint8_t *split_in;    // [256 * nbx * nby] by (t, sub): 1 = split in this frame
     uint8_t *split_out;         // ... this frame's verdicts (the lane's next frame reads them)
     const uint32_t *list_in;    // [kSplitMax] (t << 16 | sub) of split_in's ones, [kSplitMax] their
-                                // count, [kSplitMax + 1..3] the frame's W, H, nbx
+                                // count, [kSplitMax + 1..3] the frame's W, H, nbx, [kSplitMax + 4]
+                                // the longest time (s_memrealtime ticks) a workgroup of it took
     uint32_t *list_out;         // the next frame's
     uint32_t *list_reset;       // the list after it (its count is zeroed here)
     int32_t nhelp;              // helper workgroups (3 x kSplitMax)
@@ -211,12 +212,12 @@ struct DrawParams {
 #define GS_DRAW_SPLIT_MAX 1024
 #endif
 constexpr int kSplitMax = GS_DRAW_SPLIT_MAX;  // split sub-blocks per frame at most (3 helpers each)
-// GS_DRAW_SPLIT > 0: sub-blocks whose previous frame (on the lane) batched at least that many box
-// survivors are blended as four 8x8 quadrants by four workgroups (k_draw: quad); 0: off
+// GS_DRAW_SPLIT > 0: sub-blocks that took at least GS_DRAW_SPLIT % of the longest workgroup time of
+// the lane's previous frame are blended as four 8x8 quadrants by four workgroups (k_draw: quad); 0: off
 #ifndef GS_DRAW_SPLIT
 #define GS_DRAW_SPLIT 0
 #endif
-constexpr int kSplitListWords = kSplitMax + 4;
+constexpr int kSplitListWords = kSplitMax + 8;
 
 // radix sort scratch (gs_sort.hip)
 struct SortScratch {

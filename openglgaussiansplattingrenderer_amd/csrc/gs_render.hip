@@ -1571,6 +1571,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     if (kSplit && P.split_in) {
         if (L == 0 && threadIdx.x == 0) {  // this frame's list is empty; the one after next starts empty
             P.list_reset[kSplitMax] = 0u;
+            P.list_reset[kSplitMax + 4] = 0u;
             P.list_out[kSplitMax + 1] = (uint32_t)P.W;
             P.list_out[kSplitMax + 2] = (uint32_t)P.H;
             P.list_out[kSplitMax + 3] = (uint32_t)P.nbx;
@@ -1588,9 +1589,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         L -= P.nhelp;
     }
     // a sub-block's workgroup: its split verdict for the lane's next frame -- heavy ones join that
-    // frame's helper list (at most kSplitMax; a sub-block is split iff it is in the list)
-    auto finish_block = [&](bool heavy) __attribute__((always_inline)) {
-        if (!kSplit || !P.split_in || helper) return;
+    // frame's helper list (at most kSplitMax; a sub-block is split iff it is in the list).  Heavy =
+    // it took at least GS_DRAW_SPLIT % of the longest time a workgroup of the lane's previous frame
+    // took (a quadrant: a third of that); every workgroup also records its time for the next frame.
+    const uint64_t t_blk = kSplit ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    auto finish_block = [&](bool) __attribute__((always_inline)) {
+        if (!kSplit || !P.split_in) return;
+        const uint32_t dur = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - t_blk, 0xffffffffull);
+        const uint64_t mx = split_on ? (uint64_t)P.list_in[kSplitMax + 4] : 0ull;
+        const bool heavy = mx != 0 && (uint64_t)dur * 100u * (quad < 0 ? 1u : 3u) >= mx * (uint64_t)GS_DRAW_SPLIT;
+        if (threadIdx.x == 0) atomicMax(&P.list_out[kSplitMax + 4], dur);
+        if (helper) return;
         if (threadIdx.x == 0) {
             bool in = false;
             if (heavy) {
@@ -1637,7 +1646,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
     const int x0 = P.xb[tx] + sbx * SB, y0 = P.yb[ty] + sby * SB;
     if (x0 >= xe || y0 >= ye) {  // uniform: sub-block beyond this tile
-        finish_block(false);
+        finish_block(false);  // (records its time; a time this short is never heavy)
         return;
     }
     const int x1 = min(x0 + SB, xe), y1 = min(y0 + SB, ye);
@@ -1796,7 +1805,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     uint32_t qn = 0;            // survivors queued (uniform)
     bool inflight = false;      // a batch's data gather is in flight (uniform)
     uint32_t nsurv = 0, prio = 0;  // GS_DRAW_PRIO: box survivors batched so far, the wave's priority
-    uint32_t nsurv_all = 0;        // GS_DRAW_SPLIT: box survivors batched (this frame's verdict)
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -1847,7 +1855,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         Dd = SurvData{ld.mx, ld.my, ld.a, ld.b, ld.c, ld.o, 0.0f};  // thr: once the data arrived (blend_batch)
         Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
         bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
-        if (kSplit) nsurv_all += bn;
         if (GS_DRAW_PRIO) {  // (see GS_DRAW_PRIO) the wave's issue priority by the survivors it took on
             nsurv += bn;
             const uint32_t lvl = min(3u, nsurv / (uint32_t)(GS_DRAW_PRIO + 0));
@@ -2206,9 +2213,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         if (wr && qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
     }
     }
-    // the verdict for the lane's next frame: split when this sub-block took on GS_DRAW_SPLIT box
-    // survivors or more (a quadrant of a split one: half that -- a quadrant sees about half)
-    finish_block(quad < 0 ? nsurv_all >= (uint32_t)GS_DRAW_SPLIT : nsurv_all >= (uint32_t)GS_DRAW_SPLIT / 2);
+    finish_block(true);  // the verdict for the lane's next frame
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x < (unsigned)kDrawTraceBlocks) {
@@ -2217,9 +2222,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
             tr[1] = (uint32_t)t1;
             tr[2] = (uint32_t)st_iter;
             tr[3] = (uint32_t)st_surv;
-            tr[4] = (uint32_t)st_kit;
-            tr[5] = (uint32_t)st_anyneed;
-            tr[6] = (uint32_t)st_pxneed;
+            // (the light trace: the split form instead -- quadrant + 2 (1: whole), the helper list's
+            // count as read, whether the list matched the frame)
+            tr[4] = STATS_FULL ? (uint32_t)st_kit : (uint32_t)(quad + 2);
+            tr[5] = STATS_FULL ? (uint32_t)st_anyneed : (kSplit && P.split_in ? P.list_in[kSplitMax] : 0u);
+            tr[6] = STATS_FULL ? (uint32_t)st_pxneed : (uint32_t)split_on;
             tr[7] = (uint32_t)max(0, end - start);
             tr[8] = (uint32_t)st_kit64;
             tr[9] = (uint32_t)st_kit128;

@@ -48,6 +48,12 @@ print("resident blocks at 5% steps:", act)
 o = np.argsort(-d)[:8]
 for i in o:
     print(f"  long block: {d[i]:.1f} us start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]}")
+if os.environ.get("GS_LIGHT_TRACE"):  # (GS_DRAW_LIGHT_TRACE builds: tr[4] quadrant + 2, tr[5] list count, tr[6] list valid)
+    q = tr[:, 4]
+    print("split form: whole", int((q == 1).sum()), "quadrants", [int((q == k).sum()) for k in (2, 3, 4, 5)],
+          "list counts seen", sorted(set(tr[:, 5].tolist()))[:8], "list valid", sorted(set(tr[:, 6].tolist())))
+    for i in o:
+        print(f"  long block {i}: quad {q[i] - 2}")
 A = np.stack([tr[:, 2], tr[:, 3], np.ones(len(tr))], 1).astype(float)
 coef, *_ = np.linalg.lstsq(A, d, rcond=None)
 print(f"duration ~ {coef[0]:.3f} us/iteration + {coef[1]:.3f} us/survivor + {coef[2]:.1f} us")
