@@ -131,6 +131,9 @@ constexpr uint32_t kPrefixDepthSlack = GS_PREFIX_SLACK;
 #endif
 // a turned frame's class target: GS_PREFIX_TURN_MUL x the neighbourhood's depth + its slack x
 // GS_PREFIX_TURN_SLACK_MUL
+#ifndef GS_PREFIX_RECT_SLACK  // a turned frame's slack (x kPrefixDepthSlack) with source rectangles
+#define GS_PREFIX_RECT_SLACK 2u
+#endif
 #ifndef GS_PREFIX_TURN_MUL
 #define GS_PREFIX_TURN_MUL 2u
 #endif

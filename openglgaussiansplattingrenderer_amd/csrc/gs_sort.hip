@@ -1149,7 +1149,9 @@ __global__ __launch_bounds__(256) void k_prefix_select(PrefixDev pre, TileRects 
                 if (x >= 0 && x < 16 && y >= 0 && y < 16) dep_nb = max(dep_nb, pre.depth[y * 16 + x]);
             }
     }
-    const uint32_t slack_nb = (GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack) * GS_PREFIX_TURN_SLACK_MUL;
+    // (the source rectangles: GS_PREFIX_RECT_SLACK x the slack; the 3 x 3 neighbourhood: twice it)
+    const uint32_t slack_nb = use_rects ? GS_PREFIX_RECT_SLACK * kPrefixDepthSlack
+                                        : (GS_PREFIX_TURN_NB == 1 ? 2 * kPrefixDepthSlack : kPrefixDepthSlack) * GS_PREFIX_TURN_SLACK_MUL;
 #pragma unroll
     for (int cp = 0; cp < kPrefixHistCopies; ++cp) {
         uint32_t *h = pre.hist + ((size_t)cp * 256 + c) * kPrefixBuckets;

@@ -20,4 +20,7 @@ for v in $TL; do
   head -6 gpurun_out/timeline_$v.txt
 done
 cp /tmp/orig.so $L/libgsplat_hip.so
-[ $# -gt 0 ] && bash tools/ab_variants.sh "$@"
+[ $# -gt 0 ] && { bash tools/ab_variants.sh "$@" || exit 1; }
+# SWEEPV="a b": a second same-box A/B of those variants with the camera sweeps
+[ -n "$SWEEPV" ] && SWEEP=1 bash tools/ab_variants.sh $SWEEPV
+exit 0
