@@ -38,6 +38,8 @@ extern "C" {
 #define GS_FLAG_TIMING 4u    /* record per-stage hipEvent timings into gs_frame_stats */
 #define GS_FLAG_NO_CULL 8u   /* disable the (exactness-preserving) per-block entry cull */
 #define GS_FLAG_DRAW_STATS 16u /* count blend work (see gs_draw_stats); slower, diagnostics only */
+#define GS_FLAG_DRAW_TRACE 128u /* with GS_FLAG_DRAW_STATS: only per-block times, list steps, survivors
+                                  * and batches (the full counters about double the blend's span) */
 #define GS_FLAG_SH 64u       /* SURVEY f3, beyond the reference: view-dependent colour from degree-3
                               * spherical harmonics (scene needs gs_scene_set_sh); the reference
                               * reads f_rest and discards it (src/Splats.cpp:300-302) */

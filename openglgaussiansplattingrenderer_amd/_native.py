@@ -23,6 +23,7 @@ GS_FLAG_FAST_EXP = 2
 GS_FLAG_TIMING = 4
 GS_FLAG_NO_CULL = 8
 GS_FLAG_DRAW_STATS = 16
+GS_FLAG_DRAW_TRACE = 128  # with GS_FLAG_DRAW_STATS: per-block times and counts only
 GS_FLAG_SH = 64
 
 GS_READ_KEYS = 1

@@ -175,11 +175,6 @@ struct Lane {
     uint32_t *vals_base = nullptr;  // the allocation: kValsPad zero words, then vals (k_draw reads vals[-1] = 0)
     uint2 *sbox_base = nullptr;     // GS_DRAW_SBOX: splat 0's box, then the boxes by position
     int64_t sbox_cap = 0;           // ... positions it holds (allocated by the first prefix-sorted frame)
-    // GS_DRAW_SPLIT: three rotating sets of per-sub-block split verdicts (bytes, split_flags_cap each)
-    // then three helper lists (gs::kSplitListWords words each); split_seq counts the lane's draws
-    uint8_t *split_buf = nullptr;
-    size_t split_flags_cap = 0;
-    uint32_t split_seq = 0;
     bool keys_sorted = true;  // false: the frame sort left only the values sorted (gs_frame_read re-sorts)
     bool vals_partial = false;  // the frame was prefix-sorted: vals holds only each list's sorted prefix
     uint32_t *pre_buf = nullptr;  // prefix-sort state (gs::kPrefixWords words, see gs::PrefixDev)
@@ -773,7 +768,7 @@ void gs_ctx_destroy(gs_ctx *ctx) {
     for (gs_scene *sc : ctx->scenes) sc->ctx = nullptr;  // they stay valid for gs_scene_destroy
     for (Lane &ln : ctx->lane) {
         void *bufs[] = {ln.sd, ln.cullbox, ln.rec, ln.blocksum, ln.totals, ln.keys, ln.vals_base,
-                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb, ln.kdup, ln.blocksum_k, ln.sbox_base, ln.split_buf};
+                        ln.bin_counts, ln.bins, ln.img, ln.ask, ln.col, ln.pre_buf, ln.lb, ln.kdup, ln.blocksum_k, ln.sbox_base};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         gs::sort_free(ln.sort);
@@ -1316,31 +1311,7 @@ int enqueue_draw(gs_ctx *ctx, const gs_scene *scene, int width, int height, floa
     P.prefix = prefix ? 1 : 0;
     P.depth = GS_PREFIX_DEPTH ? ctx->prefix_depth : nullptr;  // (every blend of the context refreshes the per-tile depths)
     P.sbox = (GS_DRAW_SBOX && prefix) ? ctx->L->sbox_base + 1 : nullptr;
-    // GS_DRAW_SPLIT: the lane's three rotating sets of split verdicts and helper lists (gs::DrawParams)
-    P.split_in = nullptr;
-    P.nhelp = 0;
-    if (GS_DRAW_SPLIT && !small) {
-        Lane &ln = *ctx->L;
-        const size_t flags = (size_t)gs::kTiles * gs::kTiles * P.nbx * P.nby;
-        if (flags > ln.split_flags_cap) {  // (zero: no sub-block split, empty lists)
-            const size_t fb = (flags + 15) & ~(size_t)15;
-            const size_t bytes = 3 * (fb + gs::kSplitListWords * 4);
-            if (int rc = grow(ctx, ln.split_buf, bytes)) return rc;
-            GS_HIP(ctx, hipMemsetAsync(ln.split_buf, 0, bytes, ln.stream));
-            ln.split_flags_cap = fb;
-            ln.split_seq = 0;
-        }
-        const size_t fb = ln.split_flags_cap;
-        auto flags_of = [&](uint32_t j) { return ln.split_buf + (j % 3) * fb; };
-        auto list_of = [&](uint32_t j) { return reinterpret_cast<uint32_t *>(ln.split_buf + 3 * fb) + (j % 3) * gs::kSplitListWords; };
-        const uint32_t j = ln.split_seq++;
-        P.split_in = flags_of(j);
-        P.split_out = flags_of(j + 1);
-        P.list_in = list_of(j);
-        P.list_out = list_of(j + 1);
-        P.list_reset = list_of(j + 2);
-        P.nhelp = 3 * gs::kSplitMax;
-    }
+    P.light_trace = (flags & GS_FLAG_DRAW_TRACE) ? 1 : 0;
     // GS_FLAG_SH frames blend the colours their preprocess evaluated
     const float4 *colour = (ctx->flags & GS_FLAG_SH) ? ctx->L->col : scene->colour;
     // Blends into one output land in frame order: wait for the frames in flight on other

@@ -195,32 +195,11 @@ struct DrawParams {
     int32_t V;                  // splats with entries (when count is null; else count[0])
     int32_t prefix;             // prefix-sorted frame: windows end at bins[kBinsLimit + t] (a miss flags fr.h_totals[2])
     uint32_t *depth;            // [256] or null: each block atomicMax-es the window depth it reached (PrefixDev::depth)
-    const uint2 *sbox;          // GS_DRAW_SBOX: the frame's cull boxes by position (sbox[-1]: an empty box), or null
+    const uint2 *sbox;          // GS_DRAW_SBOX: the frame's cull boxes by position (sbox[-1]: splat 0's box), or null
+    int32_t light_trace;        // GS_FLAG_DRAW_TRACE: the STATS form records per-block times and counts only
     int32_t xb[kTiles + 1];     // pixel x range of tile column t: [xb[t], xb[t+1])
     int32_t yb[kTiles + 1];
-    // GS_DRAW_SPLIT (k_draw): the heaviest sub-blocks of the lane's previous frame blended as four
-    // 8x8 quadrants -- their own workgroup and three helpers at the front of the grid -- or null
-    // Three buffers per lane, rotating: frame j reads set j % 3 (written by the lane's frame j - 1),
-    // writes set (j + 1) % 3 (emptied by frame j - 1) and empties set (j + 2) % 3.
-    const uint8_t *split_in;    // [256 * nbx * nby] by (t, sub): 1 = split in this frame
-    uint8_t *split_out;         // ... this frame's verdicts (the lane's next frame reads them)
-    const uint32_t *list_in;    // [kSplitMax] (t << 16 | sub) of split_in's ones, [kSplitMax] their
-                                // count, [kSplitMax + 1..3] the frame's W, H, nbx, [kSplitMax + 4]
-                                // the longest time (s_memrealtime ticks) a workgroup of it took
-    uint32_t *list_out;         // the next frame's
-    uint32_t *list_reset;       // the list after it (its count is zeroed here)
-    int32_t nhelp;              // helper workgroups (3 x kSplitMax)
 };
-#ifndef GS_DRAW_SPLIT_MAX
-#define GS_DRAW_SPLIT_MAX 1024
-#endif
-constexpr int kSplitMax = GS_DRAW_SPLIT_MAX;  // split sub-blocks per frame at most (3 helpers each)
-// GS_DRAW_SPLIT > 0: sub-blocks that took at least GS_DRAW_SPLIT % of the longest workgroup time of
-// the lane's previous frame are blended as four 8x8 quadrants by four workgroups (k_draw: quad); 0: off
-#ifndef GS_DRAW_SPLIT
-#define GS_DRAW_SPLIT 0
-#endif
-constexpr int kSplitListWords = kSplitMax + 8;
 
 // radix sort scratch (gs_sort.hip)
 struct SortScratch {

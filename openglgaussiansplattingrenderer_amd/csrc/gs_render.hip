@@ -1513,20 +1513,6 @@ __device__ __forceinline__ int slot_y(uint32_t s) {
 #ifndef GS_CULL_SPARSE
 #define GS_CULL_SPARSE 6
 #endif
-// GS_DRAW_PRIO > 0: a sub-block's wave raises its issue priority (s_setprio 1, 2, 3) each time it
-// has batched another GS_DRAW_PRIO box survivors.  The blend's span is set by its heaviest
-// sub-blocks (the most survivors: ~0.7 us each beside six other waves of the SIMD), which start
-// with the first dispatch and finish alone: the light trace of C3 (tools/timeline.py) holds ~6,200
-// blocks resident for half the span and fewer and fewer after; the heavy waves' own pace sets the end.
-#ifndef GS_DRAW_PRIO
-#define GS_DRAW_PRIO 0
-#endif
-#ifndef GS_DRAW_SWALK
-#define GS_DRAW_SWALK 0
-#endif
-#ifndef GS_DRAW_LIGHT_TRACE
-#define GS_DRAW_LIGHT_TRACE 0
-#endif
 #ifndef GS_DRAW_WAVES
 #define GS_DRAW_WAVES 7
 #endif
@@ -1545,9 +1531,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // pixel state, pixel id = 16*y + x in the sub-block; a pixel is done (:129-133) iff its
     // w >= 0.99 (pixels outside the image start at w = 1)
     constexpr int SB = SMALL ? 8 : 16;  // sub-block side
-    // GS_DRAW_LIGHT_TRACE (diagnostic builds): the STATS form records only each block's times, list
-    // steps, survivors and batches -- the per-survivor counters roughly doubled the kernel's span
-    constexpr bool STATS_FULL = STATS && !GS_DRAW_LIGHT_TRACE;
+    // GS_FLAG_DRAW_TRACE (P.light_trace): the STATS form records only each block's times, list steps,
+    // survivors and batches -- the per-survivor counters roughly double the kernel's span
+    const bool STATS_FULL = STATS && !P.light_trace;
     __shared__ float4 s_col[SMALL ? 1 : 256];
     // one survivor's blend events: power and pixel id (split); 5760 B of LDS per wave in all
     // -> 7 waves/SIMD
@@ -1556,62 +1542,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     // box survivors queued in list order until a batch is blended (at most kBatch - 1 + 64 queued)
     __shared__ uint32_t s_q[GS_DRAW_BATCH + 64];
     const int nsub = P.nbx * P.nby;
-    int L = blockIdx.x;
-    // GS_DRAW_SPLIT: the sub-blocks the lane's previous frame found heaviest are blended as four 8x8
-    // quadrants (one pixel per lane, the sparse step from the start): quadrant 0 by the sub-block's
-    // own workgroup, 1-3 by helper workgroups at the front of the grid (dispatched first).  Any
-    // split gives the same pixels: each pixel still blends its own tile's list in order.
-    constexpr bool kSplit = !SMALL && GS_DRAW_SPLIT > 0;
-    int quad = -1;          // the quadrant this workgroup blends, -1: the whole sub-block (uniform)
-    int t = 0, sub = 0;
-    bool helper = false;
-    // the helper list belongs to a frame of this size (else no sub-block is split)
-    const bool split_on = kSplit && P.split_in && P.list_in[kSplitMax + 1] == (uint32_t)P.W &&
-                          P.list_in[kSplitMax + 2] == (uint32_t)P.H && P.list_in[kSplitMax + 3] == (uint32_t)P.nbx;
-    if (kSplit && P.split_in) {
-        if (L == 0 && threadIdx.x == 0) {  // this frame's list is empty; the one after next starts empty
-            P.list_reset[kSplitMax] = 0u;
-            P.list_reset[kSplitMax + 4] = 0u;
-            P.list_out[kSplitMax + 1] = (uint32_t)P.W;
-            P.list_out[kSplitMax + 2] = (uint32_t)P.H;
-            P.list_out[kSplitMax + 3] = (uint32_t)P.nbx;
-        }
-        if (L < P.nhelp) {  // uniform: a helper
-            const uint32_t e = (uint32_t)L / 3u;
-            if (!split_on || e >= min(P.list_in[kSplitMax], (uint32_t)kSplitMax)) return;
-            const uint32_t ts = P.list_in[e];
-            t = (int)(ts >> 16);
-            sub = (int)(ts & 0xffffu);
-            if (t >= kTiles * kTiles || sub >= nsub) return;
-            quad = L % 3 + 1;
-            helper = true;
-        }
-        L -= P.nhelp;
-    }
-    // a sub-block's workgroup: its split verdict for the lane's next frame -- heavy ones join that
-    // frame's helper list (at most kSplitMax; a sub-block is split iff it is in the list).  Heavy =
-    // it took at least GS_DRAW_SPLIT % of the longest time a workgroup of the lane's previous frame
-    // took (a quadrant: a third of that); every workgroup also records its time for the next frame.
-    const uint64_t t_blk = kSplit ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    auto finish_block = [&](bool) __attribute__((always_inline)) {
-        if (!kSplit || !P.split_in) return;
-        const uint32_t dur = (uint32_t)min(__builtin_amdgcn_s_memrealtime() - t_blk, 0xffffffffull);
-        const uint64_t mx = split_on ? (uint64_t)P.list_in[kSplitMax + 4] : 0ull;
-        const bool heavy = mx != 0 && (uint64_t)dur * 100u * (quad < 0 ? 1u : 3u) >= mx * (uint64_t)GS_DRAW_SPLIT;
-        if (threadIdx.x == 0) atomicMax(&P.list_out[kSplitMax + 4], dur);
-        if (helper) return;
-        if (threadIdx.x == 0) {
-            bool in = false;
-            if (heavy) {
-                const uint32_t i = atomicAdd(&P.list_out[kSplitMax], 1u);
-                if (i < (uint32_t)kSplitMax) {
-                    P.list_out[i] = ((uint32_t)t << 16) | (uint32_t)sub;
-                    in = true;
-                }
-            }
-            P.split_out[t * nsub + sub] = in ? 1 : 0;
-        }
-    };
+    const int L = blockIdx.x;
     if (L >= kTiles * kTiles * nsub) {  // uniform: a margin block -- zero pixels outside the
         // drawn coverage (Q9: the reference dispatches (W/32)x(H/32) groups of 32x32); done here
         // instead of a memset launch
@@ -1634,21 +1565,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         }
         return;
     }
-    if (!helper) {
-        const int xcd = L & 7, kk = L >> 3;
-        // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
-        t = (int)bins[256 + xcd + 8 * (kk / nsub)];
-        sub = kk - (kk / nsub) * nsub;
-        if (split_on && P.split_in[t * nsub + sub]) quad = 0;
-    }
+    const int xcd = L & 7, kk = L >> 3;
+    // coarse tile: the (xcd + 8*(kk/nsub))-th longest (bins[256..]); its rank % 8 == xcd
+    const int t = (int)bins[256 + xcd + 8 * (kk / nsub)];
+    const int sub = kk - (kk / nsub) * nsub;
     const int tx = t & 15, ty = t >> 4;
     const int sby = sub / P.nbx, sbx = sub - sby * P.nbx;
     const int xe = P.xb[tx + 1], ye = P.yb[ty + 1];
     const int x0 = P.xb[tx] + sbx * SB, y0 = P.yb[ty] + sby * SB;
-    if (x0 >= xe || y0 >= ye) {  // uniform: sub-block beyond this tile
-        finish_block(false);  // (records its time; a time this short is never heavy)
-        return;
-    }
+    if (x0 >= xe || y0 >= ye) return;  // uniform: sub-block beyond this tile
     const int x1 = min(x0 + SB, xe), y1 = min(y0 + SB, ye);
     const int lane = threadIdx.x;
     const int pxa = x0 + 2 * (lane & 7), pya = y0 + 2 * (lane >> 3);
@@ -1677,11 +1602,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     const int wend = end;
     if (P.prefix) end = min(end, (int)min(bins[kBinsLimit + t], 0x7fffffffu));
     const int qmax = max(E - 1, 0);
-    // pixels outside the image count as done (and, split, those of the other quadrants: a lane's
-    // 2x2 quad lies in one quadrant)
-    const int lquad = ((lane & 7) >= 4 ? 1 : 0) + ((lane >> 3) >= 4 ? 2 : 0);
-    const bool mine = !kSplit || quad < 0 || lquad == quad;
-    bool d00 = !in00 || !mine, d10 = !in10 || !mine, d01 = !in01 || !mine, d11 = !in11 || !mine;
+    // pixels outside the image count as done
+    bool d00 = !in00, d10 = !in10, d01 = !in01, d11 = !in11;
 #if GS_DRAW_LANEMAJOR
     // the pixel states are lane-major: the state of the lane's value k (pixel (pxa + k % 2,
     // pya + k / 2)) is slot 64 k + lane -- a value's events, taken in lane order, read and write
@@ -1804,7 +1726,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     bool cfin = true;           // every colour of the batch is finite (uniform)
     uint32_t qn = 0;            // survivors queued (uniform)
     bool inflight = false;      // a batch's data gather is in flight (uniform)
-    uint32_t nsurv = 0, prio = 0;  // GS_DRAW_PRIO: box survivors batched so far, the wave's priority
 
     // Indices are loaded clamped to the list, so every loaded value is a valid splat id and
     // is used as loaded (a select on it right after the load would wait for the load);
@@ -1855,16 +1776,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
         Dd = SurvData{ld.mx, ld.my, ld.a, ld.b, ld.c, ld.o, 0.0f};  // thr: once the data arrived (blend_batch)
         Dc = *at(reinterpret_cast<const SurvRgb *>(colour), id << 4);
         bk = bn >= 64u ? ~0ull : ((1ull << bn) - 1ull);
-        if (GS_DRAW_PRIO) {  // (see GS_DRAW_PRIO) the wave's issue priority by the survivors it took on
-            nsurv += bn;
-            const uint32_t lvl = min(3u, nsurv / (uint32_t)(GS_DRAW_PRIO + 0));
-            if (lvl != prio) {  // uniform, at most three times per block
-                prio = lvl;
-                if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-                else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-                else __builtin_amdgcn_s_setprio(3);
-            }
-        }
         if (qn > 64u) {  // uniform, rare
             const uint32_t r = s_q[64 + lane];
             wave_lds_sync();
@@ -2126,32 +2037,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
     };
     // prologue: chunk 0 index-loaded and box-gathered, chunk 1 index-loaded
     int base = start;
-    if (SBOX && GS_DRAW_SWALK && base < end && !all_done) {  // uniform
-        // the positional walk (sorted boxes): a chunk's index and box loads depend only on its
-        // position, so both issue two steps before its test (the gather form issues the box one
-        // step before: it needs the index)
-        auto load_pos = [&](int b, uint32_t &v, uint2 &bx) {
-            uint32_t off;
-            load_idx(b, v, off);
-            bx = *at(box_base, off << 3);
-        };
-        load_pos(base, Vi[0], Bx[0]);
-        load_pos(base + 64, Vi[1], Bx[1]);
-        auto step = [&](auto U) {
-            constexpr int u = decltype(U)::value;
-            test_and_queue(base, min(Vi[u], idmax), Bx[u]);  // chunk c
-            load_pos(base + 128, Vi[u], Bx[u]);              // chunk c+2
-            if (STATS) ++st_iter;
-            if (inflight) blend_batch();
-            base += 64;
-            if (qn >= kBatch || (base >= end && qn)) issue_batch();  // uniform
-            return (base < end || inflight) && !all_done;
-        };
-        for (;;) {
-            if (!step(std::integral_constant<int, 0>{})) break;
-            if (!step(std::integral_constant<int, 1>{})) break;
-        }
-    } else if (base < end && !all_done) {  // uniform
+    if (base < end && !all_done) {  // uniform
         uint32_t v0, o0;
         load_idx(base, v0, o0);
         load_idx(base + 64, Vi[1], Oi[1]);
@@ -2199,34 +2085,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GS_DRAW_WAVE
        // spilled there, a private segment in the dominant kernel)
         const int l2 = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         const int qx = x0 + 2 * (l2 & 7), qy = y0 + 2 * (l2 >> 3);
-        // (split: only this workgroup's quadrant)
-        const bool wr = !kSplit || quad < 0 || (((l2 & 7) >= 4 ? 1 : 0) + ((l2 >> 3) >= 4 ? 2 : 0)) == quad;
 #if GS_DRAW_LANEMAJOR
         const int qb = l2, q1 = 64, q2 = 128, q3 = 192;
 #else
         const int qb = 32 * (l2 >> 3) + 2 * (l2 & 7), q1 = 1, q2 = 16, q3 = 17;
 #endif
         uint32_t *row0 = out + (size_t)qy * P.W + qx, *row1 = row0 + P.W;
-        if (wr && qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
-        if (wr && qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + q1]);
-        if (wr && qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + q2]);
-        if (wr && qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
+        if (qx < x1 && qy < y1) row0[0] = pack_rgba8(s_col[qb + 0]);
+        if (qx + 1 < x1 && qy < y1) row0[1] = pack_rgba8(s_col[qb + q1]);
+        if (qx < x1 && qy + 1 < y1) row1[0] = pack_rgba8(s_col[qb + q2]);
+        if (qx + 1 < x1 && qy + 1 < y1) row1[1] = pack_rgba8(s_col[qb + q3]);
     }
     }
-    finish_block(true);  // the verdict for the lane's next frame
     if (STATS && lane == 0) {  // one plain record per block (no contended atomics)
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        if (blockIdx.x < (unsigned)kDrawTraceBlocks) {
-            uint32_t *tr = reinterpret_cast<uint32_t *>(stats) + kDrawTraceWords * blockIdx.x;
+        if (L < kDrawTraceBlocks) {
+            uint32_t *tr = reinterpret_cast<uint32_t *>(stats) + kDrawTraceWords * L;
             tr[0] = (uint32_t)st_t0;
             tr[1] = (uint32_t)t1;
             tr[2] = (uint32_t)st_iter;
             tr[3] = (uint32_t)st_surv;
-            // (the light trace: the split form instead -- quadrant + 2 (1: whole), the helper list's
-            // count as read, whether the list matched the frame)
-            tr[4] = STATS_FULL ? (uint32_t)st_kit : (uint32_t)(quad + 2);
-            tr[5] = STATS_FULL ? (uint32_t)st_anyneed : (kSplit && P.split_in ? P.list_in[kSplitMax] : 0u);
-            tr[6] = STATS_FULL ? (uint32_t)st_pxneed : (uint32_t)split_on;
+            tr[4] = (uint32_t)st_kit;
+            tr[5] = (uint32_t)st_anyneed;
+            tr[6] = (uint32_t)st_pxneed;
             tr[7] = (uint32_t)max(0, end - start);
             tr[8] = (uint32_t)st_kit64;
             tr[9] = (uint32_t)st_kit128;
@@ -2353,7 +2234,7 @@ void launch_draw(hipStream_t s, const DrawParams &P, bool fast_exp, bool small, 
     // (see k_draw), then the margin blocks (256 uncovered pixels each); with no coverage only
     // margin blocks run
     const int margin = P.W * P.H - P.coverW * P.coverH;
-    const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256 + (P.split_in ? P.nhelp : 0), 1));
+    const dim3 grid(std::max(kTiles * kTiles * P.nbx * P.nby + (margin + 255) / 256, 1));
     // (GS_DRAW_SBOX off: the sorted boxes are never set, see the frame paths)
     auto go = [&](auto kern) {
         hipExtLaunchKernelGGL(kern, grid, dim3(64), 0, s, start, stop, 0, P, bins, vals, fr.cullbox, fr.sd, colour, out,

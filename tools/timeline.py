@@ -24,7 +24,10 @@ else:
 cam = g.main_camera(W, H)
 cam.rotateRight(45.0 * view)
 u = cam.uniforms()
-sp.flags = flags | g.GS_FLAG_DRAW_STATS
+# GS_LIGHT_TRACE=1 (environment): GS_FLAG_DRAW_TRACE -- per-block times and counts only (the full
+# per-survivor counters about double the blend's span)
+light = bool(os.environ.get("GS_LIGHT_TRACE"))
+sp.flags = flags | g.GS_FLAG_DRAW_STATS | (g.GS_FLAG_DRAW_TRACE if light else 0)
 for _ in range(3):
     sp.render_uniforms(u)
 ctx.draw_stats(reset=True)
@@ -48,12 +51,6 @@ print("resident blocks at 5% steps:", act)
 o = np.argsort(-d)[:8]
 for i in o:
     print(f"  long block: {d[i]:.1f} us start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]}")
-if os.environ.get("GS_LIGHT_TRACE"):  # (GS_DRAW_LIGHT_TRACE builds: tr[4] quadrant + 2, tr[5] list count, tr[6] list valid)
-    q = tr[:, 4]
-    print("split form: whole", int((q == 1).sum()), "quadrants", [int((q == k).sum()) for k in (2, 3, 4, 5)],
-          "list counts seen", sorted(set(tr[:, 5].tolist()))[:8], "list valid", sorted(set(tr[:, 6].tolist())))
-    for i in o:
-        print(f"  long block {i}: quad {q[i] - 2}")
 A = np.stack([tr[:, 2], tr[:, 3], np.ones(len(tr))], 1).astype(float)
 coef, *_ = np.linalg.lstsq(A, d, rcond=None)
 print(f"duration ~ {coef[0]:.3f} us/iteration + {coef[1]:.3f} us/survivor + {coef[2]:.1f} us")
