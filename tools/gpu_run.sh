@@ -6,6 +6,7 @@
 #   ab K [ARGS] tests -k K on the working tree's library, then bench A (lib/libgsplat_hip_old.so,
 #               tools/build_ab.sh) / B (the working tree's) twice each, interleaved
 #   variants N.. same-box A/B of lib/variants/N.so (tools/variants.sh)
+#   lab V..     experiments: TESTV / TL / SWEEPV (see the mode) and a same-box A/B of lib/variants/V.so
 #   configs     bench lines of C4, SH, clean, fast exp, C2 and the eight C5 views
 #   profiles T  the round's rocprofv3 collection (trace by pass, FETCH / WRITE / SQ, C2, view 4)
 set -o pipefail
@@ -54,6 +55,28 @@ for k, r in sw.items():
 variants)
   # same-box A/B of lib/variants/NAME.so builds (tools/variants.sh NAME -DFLAG=...), in the given order, twice
   bash tools/ab_variants.sh "$@" ;;
+lab)
+  # experiment runs: TESTV=NAME every GPU test on lib/variants/NAME.so; TL="a b" light-trace
+  # timelines (tools/timeline.py, GS_FLAG_DRAW_TRACE) of those variants; then a same-box A/B of the
+  # variants given as arguments (tools/ab_variants.sh) and SWEEPV="a b" another with the camera sweeps
+  L=openglgaussiansplattingrenderer_amd/lib
+  cp $L/libgsplat_hip.so /tmp/orig.so
+  if [ -n "$TESTV" ]; then
+    cp $L/variants/$TESTV.so $L/libgsplat_hip.so
+    timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $O/tests_$TESTV.log 2>&1
+    rc=$?; tail -2 $O/tests_$TESTV.log
+    cp /tmp/orig.so $L/libgsplat_hip.so
+    [ $rc -eq 0 ] || { grep -E "FAILED|Error" $O/tests_$TESTV.log | head -5; exit 1; }
+  fi
+  for v in $TL; do
+    cp $L/variants/$v.so $L/libgsplat_hip.so
+    GS_LIGHT_TRACE=1 timeout -k 10 200 python tools/timeline.py c3 > $O/timeline_$v.txt 2>&1 || { cp /tmp/orig.so $L/libgsplat_hip.so; exit 1; }
+    sed -n 3,6p $O/timeline_$v.txt
+  done
+  cp /tmp/orig.so $L/libgsplat_hip.so
+  [ $# -gt 0 ] && { bash tools/ab_variants.sh "$@" || exit 1; }
+  [ -n "$SWEEPV" ] && SWEEP=1 bash tools/ab_variants.sh $SWEEPV
+  exit 0 ;;
 configs)
   # bench lines of the other configs / modes and every C5 view (pose k), one GPU -> gpurun_out/configs/
   C=$O/configs; mkdir -p $C
