@@ -472,7 +472,7 @@ gs::SceneDev scene_dev(const gs_scene *s) {
     d.mx = s->soa;
     d.my = s->soa + n;
     d.mz = s->soa + 2 * n;
-    d.shape = reinterpret_cast<const float4 *>(s->soa + gs::scene_shape_offset(n));
+    d.shape = s->soa + gs::scene_shape_offset(n);
     d.colour = s->colour;
     d.sh = s->sh;
     return d;
@@ -912,8 +912,8 @@ int gs_scene_create(gs_ctx *ctx, int n, const float *means4, const float *cov6, 
         soa[i] = means4[4 * i + 0];
         soa[nn + i] = means4[4 * i + 1];
         soa[2 * nn + i] = means4[4 * i + 2];
-        for (int c = 0; c < 6; ++c) shape[8 * i + c] = cov6[6 * i + c];
-        shape[8 * i + 6] = opacity[i];
+        for (int c = 0; c < 6; ++c) shape[gs::kShapeFloats * i + c] = cov6[6 * i + c];
+        shape[gs::kShapeFloats * i + 6] = opacity[i];
     }
     gs_scene *s = new gs_scene();
     s->ctx = ctx;
@@ -1046,8 +1046,8 @@ int gs_scene_download(const gs_scene *scene, float *means4, float *cov6, float *
             means4[4 * i + 3] = 1.f;
         }
         if (cov6)
-            for (int c = 0; c < 6; ++c) cov6[6 * i + c] = shape[8 * i + c];
-        if (opacity) opacity[i] = shape[8 * i + 6];
+            for (int c = 0; c < 6; ++c) cov6[6 * i + c] = shape[gs::kShapeFloats * i + c];
+        if (opacity) opacity[i] = shape[gs::kShapeFloats * i + 6];
     }
     return GS_OK;
 }

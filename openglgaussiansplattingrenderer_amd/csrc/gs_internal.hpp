@@ -251,15 +251,21 @@ void launch_gather_keys(hipStream_t s, const float *keys, const int32_t *order, 
 
 // render kernels (gs_render.hip)
 // The scene on the device (gs_scene::soa): the means as three planes of n floats (the
-// projection reads them for every splat), then from scene_shape_offset(n) floats on one 32-byte
-// shape record per splat, (S00, S01, S02, S11) (S12, S22, opacity, 0): two 16-byte loads, which
-// lanes of NDC-culled splats can skip whole (k_preprocess_q, LAZY), instead of seven planes
+// projection reads them for every splat), then from scene_shape_offset(n) floats on one 28-byte
+// shape record per splat, (S00, S01, S02, S11, S12, S22, opacity): a 16-byte and a 12-byte load at
+// 4-byte alignment, which lanes of NDC-culled splats can skip whole (k_preprocess_q, LAZY),
+// instead of seven planes.  40 B per splat with the means, SURVEY 8(d)'s algorithmic bytes (round
+// 6; a padded 32-byte record before: same box, alternated, preprocess 0.1142 / 0.1144 -> 0.1099 /
+// 0.1102 ms, three lanes 2375 / 2384 -> 2398 / 2399 frames/s, profiles/r06/shape28_ab.txt)
+constexpr int kShapeFloats = 7;  // floats per shape record
 __host__ __device__ inline size_t scene_shape_offset(size_t n) { return (3 * n + 3) & ~(size_t)3; }
-__host__ __device__ inline size_t scene_floats(size_t n) { return scene_shape_offset(n) + 8 * n; }
+__host__ __device__ inline size_t scene_floats(size_t n) { return scene_shape_offset(n) + kShapeFloats * n + 1; }
+typedef float f32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
 struct SceneDev {
     int n;
     const float *mx, *my, *mz;   // SoA means
-    const float4 *shape;         // [2 n]: (S00, S01, S02, S11), (S12, S22, opacity, 0) per splat
+    const float *shape;          // kShapeFloats per splat: S00, S01, S02, S11, S12, S22, opacity
     const float4 *colour;        // (r,g,b,1) 0..255 (reference colours vec4)
     const float *sh;             // degree-3 SH, 48 floats per splat, splat-major (gs_render.hip sh_quad), or null
 };

@@ -50,9 +50,10 @@ __global__ __launch_bounds__(256) void k_ply_activate(const float *__restrict__ 
 #pragma unroll
         for (int q = 0; q < 3; ++q) Sig[c][q] = M[q][0] * M[c][0] + M[q][1] * M[c][1] + M[q][2] * M[c][2];
     // the shape record (SceneDev): covariance upper triangle and opacity
-    float4 *shape = reinterpret_cast<float4 *>(soa + scene_shape_offset(nn)) + 2 * i;
-    shape[0] = make_float4(Sig[0][0], Sig[0][1], Sig[0][2], Sig[1][1]);
-    shape[1] = make_float4(Sig[1][2], Sig[2][2], opac, 0.0f);
+    float *shape = soa + scene_shape_offset(nn) + (size_t)kShapeFloats * i;
+    const float rs[kShapeFloats] = {Sig[0][0], Sig[0][1], Sig[0][2], Sig[1][1], Sig[1][2], Sig[2][2], opac};
+#pragma unroll
+    for (int c = 0; c < kShapeFloats; ++c) shape[c] = rs[c];
 }
 
 }  // namespace

@@ -46,6 +46,15 @@ __device__ __forceinline__ int f2i(float f) {
 #endif
 }
 
+// the shape record of splat i (SceneDev::shape): covariance upper triangle c0..c5 and opacity
+__device__ __forceinline__ void load_shape(const SceneDev &sc, size_t i, float &c0, float &c1, float &c2, float &c3,
+                                           float &c4, float &c5, float &op) {
+    const float *p = sc.shape + (size_t)kShapeFloats * i;
+    const f32x4_a4 a = *reinterpret_cast<const f32x4_a4 *>(p);
+    const f32x3_a4 b = *reinterpret_cast<const f32x3_a4 *>(p + 4);
+    c0 = a.x, c1 = a.y, c2 = a.z, c3 = a.w, c4 = b.x, c5 = b.y, op = b.z;
+}
+
 // glm operator*(mat4, vec4): (m0*x + m1*y) + (m2*z + m3*w)
 __device__ __forceinline__ float m4v_row(const float *m, int r, float x, float y, float z, float w) {
     return (m[0 * 4 + r] * x + m[1 * 4 + r] * y) + (m[2 * 4 + r] * z + m[3 * 4 + r] * w);
@@ -333,10 +342,7 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
     if (!valid) return make_int4(0, -1, -1, 0);
     const float mx = sc.mx[i], my = sc.my[i], mz = sc.mz[i];
     float c0, c1, c2, c3, c4, c5, opac;
-    if (!LAZY) {  // the means and the shape record in one round trip (see LAZY)
-        const float4 s0 = sc.shape[2 * (size_t)i], s1 = sc.shape[2 * (size_t)i + 1];
-        c0 = s0.x, c1 = s0.y, c2 = s0.z, c3 = s0.w, c4 = s1.x, c5 = s1.y, opac = s1.z;
-    }
+    if (!LAZY) load_shape(sc, (size_t)i, c0, c1, c2, c3, c4, c5, opac);  // the means and the shape record in one round trip (see LAZY)
     // Straight-line body: every cull folds into `vis` and the outputs are selected at the
     // end (the NDC cull splits nearly every wave, so a branch saved no work; without branches
     // all ten plane loads issue up front and no exec-mask bookkeeping runs).  Culled lanes
@@ -345,10 +351,7 @@ __device__ __forceinline__ int4 preprocess_one(const PreParams &P, const SceneDe
     const bool vis = project_ndc(P, mx, my, mz, p0, p1, p2);
     if (LAZY) {
         c0 = c1 = c2 = c3 = c4 = c5 = opac = 0.0f;
-        if (vis) {
-            const float4 s0 = sc.shape[2 * (size_t)i], s1 = sc.shape[2 * (size_t)i + 1];
-            c0 = s0.x, c1 = s0.y, c2 = s0.z, c3 = s0.w, c4 = s1.x, c5 = s1.y, opac = s1.z;
-        }
+        if (vis) load_shape(sc, (size_t)i, c0, c1, c2, c3, c4, c5, opac);
     }
     return preprocess_rest<CLEAN>(P, sc, fr, i, mx, my, mz, p0, p1, p2, vis, c0, c1, c2, c3, c4, c5, opac);
 }
@@ -627,8 +630,7 @@ __global__ __launch_bounds__(64 * kQWaves) void k_preprocess_q(PreParams P, Scen
             pi = qa_i, pp0 = qa0, pp1 = qa1, pp2 = qa2;
             if (lane < pend_n) {
                 pmx = sc.mx[pi], pmy = sc.my[pi], pmz = sc.mz[pi];
-                const float4 s0 = sc.shape[2 * (size_t)pi], s1 = sc.shape[2 * (size_t)pi + 1];
-                pc0 = s0.x, pc1 = s0.y, pc2 = s0.z, pc3 = s0.w, pc4 = s1.x, pc5 = s1.y, pop = s1.z;
+                load_shape(sc, (size_t)pi, pc0, pc1, pc2, pc3, pc4, pc5, pop);
             }
             qa_i = qb_i, qa0 = qb0, qa1 = qb1, qa2 = qb2;
             qn -= pend_n;
