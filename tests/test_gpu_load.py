@@ -56,3 +56,31 @@ def test_gpu_load_errors(tmp_path):
     with pytest.raises(g.GsError):
         g.Splats(str(tmp_path / "missing.ply"), 64, 64, ctx=ctx, gpu_load=True)
     ctx.close()
+
+
+@pytest.mark.parametrize("n", [1, 3, 4099])  # odd counts: 28-byte shape records straddle 16-byte lines
+def test_scene_roundtrip_bits(n):
+    """gs_scene_create -> gs_scene_download returns every uploaded word unchanged (mean planes and the
+    28-byte cov6 + opacity records, gs_internal.hpp kShapeFloats), including -0, subnormals, inf, NaN."""
+    ctx = g.Context(0)
+    rng = np.random.default_rng(n)
+    means = rng.integers(0, 2**32, (n, 4), dtype=np.uint32).view(np.float32).copy()
+    cov = rng.integers(0, 2**32, 6 * n, dtype=np.uint32).view(np.float32).copy()
+    op = rng.integers(0, 2**32, n, dtype=np.uint32).view(np.float32).copy()
+    col = rng.integers(0, 2**32, (n, 4), dtype=np.uint32).view(np.float32).copy()
+    special = np.array([0x80000000, 0x00000001, 0x7F800000, 0x7FC00001], np.uint32).view(np.float32)
+    cov[:min(6 * n, 4)] = special[:min(6 * n, 4)]
+    op[-1] = special[3]
+    means[0, :3] = special[:3]
+    s = g.Splats(None, 64, 64, ctx=ctx, arrays=(np.zeros((n, 4), np.float32), np.zeros((n, 4), np.float32),
+                                               np.zeros(n, np.float32), np.ones((n, 3), np.float32),
+                                               np.tile(np.float32([1, 0, 0, 0]), (n, 1))))
+    s.means3D, s.covarianceMatrices, s.opacities, s.colours = means, cov, op, col
+    s.loadToGPU(64, 64)
+    m, c, o, cl = s.download()
+    assert np.array_equal(m[:, :3].view(np.uint32), means[:, :3].view(np.uint32))
+    assert np.all(m[:, 3] == 1.0)  # w is not stored (the reference's means are homogeneous points)
+    assert np.array_equal(c.view(np.uint32), cov.view(np.uint32))
+    assert np.array_equal(o.view(np.uint32), op.view(np.uint32))
+    assert np.array_equal(cl.view(np.uint32), col.view(np.uint32))
+    ctx.close()
