@@ -70,11 +70,15 @@ short = np.argsort(d)[:5]
 for i in short:
     print(f"  short block {i}: {d[i]:.1f} us  start {s[i]:.1f} iters {tr[i, 2]} surv {tr[i, 3]} events {tr[i, 6]}")
 k64, k128, ev64, refr = tr[:, 8].sum(), tr[:, 9].sum(), tr[:, 10].sum(), tr[:, 11].sum()
-print(f"survivor steps {tr[:, 4].sum()}: with <=64 active px {k64} ({k64 / tr[:, 4].sum():.1%}), <=128 {k128}"
-      f" ({k128 / tr[:, 4].sum():.1%}); events with <=64 active {ev64} ({ev64 / tr[:, 6].sum():.1%})")
-print(f"done-mask refreshes (a pixel saturated): {refr} ({refr / max(1, tr[:, 12:15].sum()):.2f} per dense step)")
-a192, a128, a64, dev = (tr[:, k].sum() for k in (12, 13, 14, 15))
-nd = a192 + a128 + a64
-print(f"dense steps {nd}: >192 active {a192} ({a192 / nd:.1%}), 129-192 {a128} ({a128 / nd:.1%}), "
-      f"65-128 {a64} ({a64 / nd:.1%}); events per dense step {dev / nd:.1f}")
+if tr[:, 4].sum() == 0:  # a light trace (GS_LIGHT_TRACE): times, list steps and survivors only
+    print("per-survivor counters not recorded (light trace)")
+else:
+    ns, ne = tr[:, 4].sum(), max(1, tr[:, 6].sum())
+    print(f"survivor steps {ns}: with <=64 active px {k64} ({k64 / ns:.1%}), <=128 {k128}"
+          f" ({k128 / ns:.1%}); events with <=64 active {ev64} ({ev64 / ne:.1%})")
+    print(f"done-mask refreshes (a pixel saturated): {refr} ({refr / max(1, tr[:, 12:15].sum()):.2f} per dense step)")
+    a192, a128, a64, dev = (tr[:, k].sum() for k in (12, 13, 14, 15))
+    nd = max(1, a192 + a128 + a64)
+    print(f"dense steps {a192 + a128 + a64}: >192 active {a192} ({a192 / nd:.1%}), 129-192 {a128} ({a128 / nd:.1%}), "
+          f"65-128 {a64} ({a64 / nd:.1%}); events per dense step {dev / nd:.1f}")
 print("counters:", st)
